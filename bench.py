@@ -1,0 +1,189 @@
+"""bench.py — Mrays/s and ms/frame of the MI355X render path (BASELINE.json metric).
+
+A step is one frame: ray generation + trace + (N>1) RCCL gather of the row stripes to rank 0 and
+de-interleave into the 1920x1080 frame.  The frame is split across ranks (strong scaling: the
+frame size is fixed).  Inputs (scene, camera) are resident on the GPU before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config config3]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (schema in the task contract) including `roofline` for the trace
+kernel (algorithmic bytes per launch from the kernel's own work counters, SURVEY.md §8d, over the
+HIP-event-timed kernel duration) and `cpu_baseline` (the oracle restatement, single-threaded, on a
+bounded pixel sample of the same workload).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raytracer.js_amd", "python"))
+
+import rtamd  # noqa: E402  (after torch: share its HIP runtime)
+from rtamd import scenes  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# Algorithmic bytes per unit of work (canonical f64 layout).
+BYTES = dict(n_ret=48, n_slot=32, n_loc=40, n_sph=36, n_box=36, n_tri=76, n_hit=40, primary=12)
+
+
+def algorithmic_bytes(counters):
+    return sum(BYTES[k] * counters[k] for k in BYTES)
+
+
+def cpu_baseline(spec, cam, cfg, budget_s):
+    """Oracle restatement (plain C, 1 thread) on a random pixel sample; Mrays/s of traced segments."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    w, root = oracle.build_scene(spec)
+    rng = np.random.default_rng(0)
+    P = cam.width * cam.height
+    order = rng.permutation(P).astype(np.int32)
+    done, segs, t_used, chunk = 0, 0, 0.0, 2048
+    while t_used < budget_s and done < P:
+        pix = order[done:done + chunk]
+        t0 = time.perf_counter()
+        r = w.trace_frame(root, cam, cfg, pixels=pix, nthreads=1)
+        t_used += time.perf_counter() - t0
+        segs += r["counters"]["segments"]
+        done += len(pix)
+        chunk = min(chunk * 2, 65536) if t_used < budget_s / 4 else chunk
+    w.close()
+    return dict(value=segs / t_used / 1e6, unit="Mrays/s", cores=1, kind="port",
+                sample="%d random pixels of the %dx%d frame (%d segments) in %.1f s, oracle/rt_oracle.c, 1 thread"
+                       % (done, cam.width, cam.height, segs, t_used))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="config3", choices=sorted(scenes.WORKLOADS))
+    ap.add_argument("--stripe", type=int, default=8, help="rows per stripe of the row-interleaved split")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    factory, W, H, refmax = scenes.WORKLOADS[args.config]
+    spec = factory()
+    t0 = time.perf_counter()
+    scene = rtamd.build_scene(spec)
+    build_s = time.perf_counter() - t0
+    ctx = rtamd.Context(local)
+    ctx.upload(scene)
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
+    # one explicit stream for librt launches, torch copies and the collectives (the legacy NULL
+    # stream would not order against librt's non-blocking stream)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+
+    rows = int(rtamd.part_rows(H, rank, world, args.stripe).size)
+    max_rows = max(int(rtamd.part_rows(H, p, world, args.stripe).size) for p in range(world))
+    local_buf = torch.zeros((max_rows, W, 3), dtype=torch.float32, device=dev)
+    frame = torch.zeros((H, W, 3), dtype=torch.float32, device=dev) if rank == 0 else None
+    if world > 1 and rank == 0:
+        gathered = [torch.empty_like(local_buf) for _ in range(world)]
+        src = np.zeros(H, np.int64)
+        for p in range(world):
+            gr = rtamd.part_rows(H, p, world, args.stripe)
+            src[gr] = p * max_rows + np.arange(len(gr))
+        src_index = torch.from_numpy(src).to(dev)
+    else:
+        gathered, src_index = None, None
+
+    def step():
+        ctx.trace_rows_device(cam, cfg, rank, world, args.stripe, local_buf.data_ptr(), sp)
+        if world > 1:
+            dist.gather(local_buf, gathered if rank == 0 else None, dst=0)
+            if rank == 0:
+                flat = torch.stack(gathered).view(world * max_rows, W, 3)
+                torch.index_select(flat, 0, src_index, out=frame)
+        elif rank == 0:
+            frame.copy_(local_buf[:H])
+
+    # work counters of one frame (untimed STATS launch): segments and algorithmic bytes
+    _, st = ctx.trace_rows_device(cam, cfg, rank, world, args.stripe, local_buf.data_ptr(), sp, stats=True)
+    counters = st.counters()
+    ctr = torch.tensor([counters[k] for k in st.COUNTERS], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(ctr)
+    tot = dict(zip(st.COUNTERS, ctr.tolist()))
+    local_bytes = algorithmic_bytes(counters)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kt = ctx.kernel_times(args.steps)
+    k_ms = float(np.mean(kt)) if len(kt) else float("nan")
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = tot["segments"] * args.steps / elapsed / 1e6
+    achieved = local_bytes / (k_ms * 1e-3) / 1e9 if k_ms == k_ms and k_ms > 0 else None
+    roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=(achieved / HBM_PEAK_GBS) if achieved else None, traffic=None,
+                    kernel="k_trace", kernel_ms=k_ms, bytes_per_launch=local_bytes,
+                    bytes_formula="48*n_ret+32*n_slot+40*n_loc+36*n_sph+36*n_box+76*n_tri+40*n_hit+12*primary")
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_budget > 0:
+        cpu = cpu_baseline(spec, cam, cfg, args.cpu_budget)
+
+    if rank == 0:
+        rec = {
+            "metric": "Mrays/s (whole node) at 1920x1080",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 seed 42 scene, BASELINE.json %s)" % args.config,
+            "config": {"workload": args.config, "scene": spec.name, "width": W, "height": H, "refmax": refmax,
+                       "entities": int(len(spec.entities)), "octree_nodes": int(scene.n_nodes),
+                       "segments_per_frame": tot["segments"], "parallelism": "rows%d/stripe%d" % (world, args.stripe),
+                       "counters": tot, "scene_build_s": round(build_s, 3)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(rec), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

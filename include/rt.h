@@ -1,0 +1,216 @@
+/*
+ * rt.h — C ABI of the MI355X render path for raytracer.js (librt_amd.so).
+ *
+ * The reference (Dark565/raytracer.js, TypeScript) has no FFI: its render path is the method
+ * Raytracer.trace_frame() (src/raytracer.ts:308-330).  This header is the seam a host binding
+ * (the N-API addon in raytracer.js_amd/js/addon, or ctypes) calls in place of that method body:
+ *
+ *   rt_create        <- `new Raytracer(config, otree, camera, ebuffer, rng)`   src/raytracer.ts:291-298
+ *   rt_upload_scene  <- the EntityOtree the Raytracer holds (src/octree_entity.ts:27, src/octree.ts:25-126)
+ *                       flattened: nodes in DFS pre-order (children 0..7), per-node entity lists in
+ *                       EntitySet (insertion) order (src/octree_entity.ts:32-49, src/entity.ts:50-56)
+ *   rt_trace_frame   <- Raytracer.trace_frame()  src/raytracer.ts:308-330  (camera scan
+ *                       src/view/camera.ts:207-250, Ray.trace src/raytracer.ts:168-277,
+ *                       ExposureBuffer.set_color src/view/exposure_buffer.ts:68-91)
+ *   rt_destroy       <- garbage collection of the Raytracer
+ *   rt_last_error    <- the thrown JS Error's message
+ *
+ * Plain C types only (no torch / HIP types).  All functions return RT_OK (0) or a negative RT_E_*
+ * code and set a thread-local message readable with rt_last_error().  No C++ exception crosses
+ * the ABI.  A context is bound to one GPU and is not re-entrant.
+ */
+#ifndef RT_AMD_H
+#define RT_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- return codes ---------------------------------------------------------------------- */
+#define RT_OK             0
+#define RT_E_INVALID     -1   /* bad argument / malformed scene                              */
+#define RT_E_HIP         -2   /* HIP runtime error                                            */
+#define RT_E_UNSUPPORTED -3   /* feature outside the parity gate (e.g. roughness > 0)         */
+#define RT_E_NOSCENE     -4   /* rt_trace_* before rt_upload_scene                            */
+#define RT_E_FAULT       -5   /* a ray reached a state where the reference throws a JS Error  */
+#define RT_E_NODEVICE    -6   /* no HIP device                                                */
+#define RT_E_TREE        -7   /* octree growth error (reference TreeOutsideGrowError /
+                                 "Node index out of range"), builder only                      */
+
+/* ---- scene ----------------------------------------------------------------------------- */
+/* Entity kinds.  SPHERE = SphereEntity (src/entities/entity_sphere.ts:29-102), BOX = BoxEntity
+ * (src/entities/entity_box.ts:29-108), FACE = the triangle entity that fills the reference's
+ * empty stub src/entities/entity_face.ts:17 (definition frozen in DESIGN.md §Triangle). */
+#define RT_ENT_SPHERE 0
+#define RT_ENT_BOX    1
+#define RT_ENT_FACE   2
+
+/* ResponseType (src/material.ts:22-26). */
+#define RT_RESP_REFLECTION   0
+#define RT_RESP_TRANSMISSION 1
+#define RT_RESP_BOTH         2
+
+/* One (Material, SolidTexture) pair as seen by an entity: StaticMaterial fields
+ * (src/material.ts:67-103) + the texture's solid colour (src/texture/texture_solid.ts:33-35). */
+typedef struct rt_shade {
+    int32_t response;    /* RT_RESP_*                                */
+    int32_t light;       /* StaticMaterial.light_source              */
+    int32_t mirror;      /* StaticMaterial.mirror                    */
+    int32_t pad_;
+    double  roughness;   /* StaticMaterial.roughness_index (must be 0 for rt_trace_*; see RT_E_UNSUPPORTED) */
+    double  rgb[3];      /* SolidTexture colour (alpha is never read on the path) */
+} rt_shade;
+
+/* Per-entity geometry, 9 doubles (ent_geom[9*i .. 9*i+8]):
+ *   SPHERE: pos.xyz, diameter, sphere_math._dot_pp, sphere_math._radius_sq, entity._radius_sq, 0, 0
+ *           (src/entities/entity_sphere.ts:34-39 and src/math/intersection.ts:94-97; the two
+ *           radius-squared caches are carried separately because the reference computes them
+ *           differently: (d/2)*(d/2) versus d*d/4)
+ *   BOX:    pos.xyz, size, 0...          (pos is the Box centre for intersection and the min corner
+ *                                          for is_within — reference inconsistency kept)
+ *   FACE:   v0.xyz, v1.xyz, v2.xyz
+ */
+typedef struct rt_scene_desc {
+    int32_t n_nodes;              /* >= 1; node 0 is the root                                  */
+    int32_t n_list;               /* total length of all per-node entity lists                 */
+    int32_t n_entities;
+    int32_t n_shades;
+    int32_t n_substances;
+    int32_t pad_;
+    const double  *node_pos;      /* [n_nodes*3]  OctreeDim.pos                                */
+    const double  *node_size;     /* [n_nodes]    OctreeDim.size                               */
+    const int32_t *node_parent;   /* [n_nodes]    -1 for the root                              */
+    const int32_t *node_child;    /* [n_nodes*8]  child node index or -1 (empty octant)        */
+    const int32_t *node_ent_begin;/* [n_nodes]    offset into list_entity                      */
+    const int32_t *node_ent_count;/* [n_nodes]                                                 */
+    const int32_t *list_entity;   /* [n_list]     entity ids, EntitySet insertion order        */
+    const int32_t *ent_type;      /* [n_entities] RT_ENT_*                                     */
+    const double  *ent_geom;      /* [n_entities*9]                                            */
+    const int32_t *ent_shade;     /* [n_entities] index into shades                            */
+    const int32_t *ent_substance; /* [n_entities] index into substance_ri, -1 = undefined      */
+    const rt_shade *shades;       /* [n_shades]                                                */
+    const double  *substance_ri;  /* [n_substances] Substance.refractive_index (src/substance.ts) */
+} rt_scene_desc;
+
+/* ---- per-frame inputs -------------------------------------------------------------------- */
+/* Camera state exactly as the reference Camera holds it (src/view/camera.ts:50-59): position,
+ * the orthonormal basis, and the per-pixel scan rotations (cos, sin) computed by the HOST with
+ * its own Math.cos/Math.sin (init_rot_vectors, src/view/camera.ts:77-87), so every backend
+ * consumes identical bits.  Rows run over height and columns over width (the reference swaps
+ * them at src/view/camera.ts:242-249, which only agrees for square screens). */
+typedef struct rt_camera_desc {
+    int32_t width;        /* screen_w */
+    int32_t height;       /* screen_h */
+    double  pos[3];
+    double  fr[3];        /* norm_fr */
+    double  lf[3];        /* norm_lf */
+    double  up[3];        /* norm_up */
+    double  scan_h[2];    /* rot_scan_h_v = (cos, sin)(fov_h / screen_w) */
+    double  scan_v[2];    /* rot_scan_v_v = (cos, sin)(fov_v / screen_h) */
+} rt_camera_desc;
+
+/* RaytracerConfig (src/raytracer.ts:33-43) + the ExposureBuffer blend weight
+ * (col_weight, src/view/exposure_buffer.ts:53-66). */
+typedef struct rt_config_desc {
+    int32_t refmax;
+    int32_t default_substance;          /* index into substance_ri, -1 = undefined */
+    double  sky_rgb[3];                 /* SkySphere(SolidTexture) colour          */
+    double  distance_attenuation_factor;
+    double  col_weight;                 /* 1.0 after reset_exposure()              */
+} rt_config_desc;
+
+/* Work counters and timing.  Filled when a non-NULL rt_stats* is passed. */
+typedef struct rt_stats {
+    int64_t segments;   /* traced ray segments: primary + every continued bounce          */
+    int64_t n_ret;      /* nodes returned by OctreeWalker.next()                           */
+    int64_t n_slot;     /* OctreeWalker.update_next_pos() calls                             */
+    int64_t n_loc;      /* node_at_pos() descent levels (re-seats, entity_at_pos)           */
+    int64_t n_sph;      /* sphere tests                                                      */
+    int64_t n_box;      /* box tests                                                         */
+    int64_t n_tri;      /* triangle tests                                                    */
+    int64_t n_hit;      /* accepted collisions (material records read)                      */
+    int64_t primary;    /* primary rays (= pixels traced)                                    */
+    int64_t n_warn;     /* rays ended by the acute-normal warning (src/raytracer.ts:200-203) */
+    int64_t n_fault;    /* rays that reached a reference throw                              */
+    double  kernel_ms;  /* trace kernel time of this call (HIP events)                      */
+    double  frame_ms;   /* whole call, host wall                                            */
+} rt_stats;
+
+/* ---- context ------------------------------------------------------------------------------ */
+typedef struct rt_ctx rt_ctx;
+
+typedef struct rt_create_desc {
+    int32_t device;       /* HIP device ordinal */
+    int32_t flags;        /* reserved, 0        */
+} rt_create_desc;
+
+int  rt_create(const rt_create_desc *desc, rt_ctx **out);
+void rt_destroy(rt_ctx *ctx);
+const char *rt_last_error(void);
+int  rt_abi_version(void);
+
+/* Copies the scene to device memory (the caller keeps ownership of every array). */
+int  rt_upload_scene(rt_ctx *ctx, const rt_scene_desc *scene);
+
+/* Full frame, host buffers.  rgb_inout is the ExposureBuffer's Float32Array (W*H*3, row-major,
+ * interleaved RGB); it is read (when col_weight != 1) and written.  hit_entity / hit_node
+ * (W*H int32, nullable) receive the entity id / DFS node id of the primary collision, -1 for none.
+ * status (W*H uint8, nullable): 0 ok, 1 acute-normal warning, 2 fault, 3 step cap. */
+int  rt_trace_frame(rt_ctx *ctx, const rt_camera_desc *cam, const rt_config_desc *cfg,
+                    float *rgb_inout, int32_t *hit_entity, int32_t *hit_node,
+                    uint8_t *status, rt_stats *stats);
+
+/* Row-striped frame slice for multi-GPU: rows are grouped in stripes of `stripe_rows`; stripe s
+ * belongs to part (s % n_parts).  Writes this part's rows compactly (stripe order) into the
+ * DEVICE buffer d_rgb (rows_of_part * W * 3 floats, col_weight ignored: plain store) on the HIP
+ * stream `stream` (NULL = the context's stream) and returns without synchronising unless
+ * stats != NULL.  *rows_out = number of rows this part owns. */
+int  rt_trace_rows_device(rt_ctx *ctx, const rt_camera_desc *cam, const rt_config_desc *cfg,
+                          int32_t part, int32_t n_parts, int32_t stripe_rows,
+                          void *d_rgb, void *stream, int32_t *rows_out, rt_stats *stats);
+
+/* Kernel time (ms) of the last `n` trace-kernel launches issued by rt_trace_rows_device, oldest
+ * first, measured with HIP events on the launch stream.  Synchronises.  Returns count written. */
+int  rt_kernel_times(rt_ctx *ctx, double *ms_out, int32_t n);
+
+/* Debug: the sequence of walker stops (tree node id, octant; octant -1 = the tree itself) of
+ * OctreeWalker.next() (src/octree_space.ts:316-361) for one ray, run on the GPU. */
+int  rt_debug_walk(rt_ctx *ctx, const double origin[3], const double dir[3], int32_t include_undefined,
+                   int32_t max_out, int32_t *out_tree, int32_t *out_octant, int32_t *n_out);
+
+/* Debug: per-pixel primary directions (W*H*3 doubles, row-major) as the ray-generation kernel
+ * produced them for `cam` (Camera.get_dir_for_each_pixel, src/view/camera.ts:207-250). */
+int  rt_debug_camera_dirs(rt_ctx *ctx, const rt_camera_desc *cam, double *dirs_out);
+
+/* ---- host-side scene builder (native add_entity_to_octree, src/octree_entity.ts:60-188) ---- */
+typedef struct rt_builder rt_builder;
+
+typedef struct rt_entity_in {
+    int32_t type;            /* RT_ENT_*                              */
+    int32_t shade;           /* index into the shade table            */
+    int32_t substance;       /* -1 = undefined                        */
+    int32_t max_in_depth;    /* AddEntityToOctreeFlags.max_in_depth   */
+    int32_t max_out_depth;   /* AddEntityToOctreeFlags.max_out_depth  */
+    int32_t pad_;
+    double  geom[9];         /* as rt_scene_desc.ent_geom; for SPHERE only pos+diameter are read,
+                                the caches are derived as the reference constructor does */
+} rt_entity_in;
+
+int  rt_builder_create(const double root_pos[3], double root_size, rt_builder **out);
+void rt_builder_destroy(rt_builder *b);
+/* add_entity_to_octree(root, entity, {max_in_depth, max_out_depth}); *entity_id = creation index */
+int  rt_builder_add(rt_builder *b, const rt_entity_in *e, int32_t *entity_id);
+int  rt_builder_add_many(rt_builder *b, const rt_entity_in *e, int32_t n);
+/* Linearise (DFS pre-order) into `out`; shade/substance tables are passed through.  Pointers in
+ * `out` stay valid until the next rt_builder_* call on `b`. */
+int  rt_builder_desc(rt_builder *b, const rt_shade *shades, int32_t n_shades,
+                     const double *substance_ri, int32_t n_substances, rt_scene_desc *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_AMD_H */

@@ -1,0 +1,245 @@
+"""ctypes binding of oracle/build/liboracle.so — the CPU restatement of the reference path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, never by the product.  See oracle/rt_oracle.h for what it restates and how it is pinned.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "raytracer.js_amd", "python"))
+from rtamd import abi  # noqa: E402  (descriptor layouts only)
+
+LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+OCT_UNDEF = -2147483648
+FAULT = -5
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    L = C.CDLL(LIB_PATH)
+    vp, pd, pi, i = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32), C.c_int
+    L.orc_world_new.restype = vp
+    L.orc_world_free.argtypes = [vp]
+    L.orc_world_free.restype = None
+    L.orc_tree_new.argtypes = [vp, pd, C.c_double, i]
+    L.orc_tree_new.restype = vp
+    L.orc_new_subtree.argtypes = [vp, vp, i, C.POINTER(vp)]
+    L.orc_tree_get.argtypes = [vp, i, C.POINTER(vp)]
+    L.orc_tree_parent.argtypes = [vp]
+    L.orc_tree_parent.restype = vp
+    L.orc_tree_id.argtypes = [vp]
+    L.orc_tree_dims.argtypes = [vp, pd, pd]
+    L.orc_tree_dims.restype = None
+    L.orc_node_at_pos.argtypes = [vp, pd, C.POINTER(vp), C.POINTER(C.c_int)]
+    L.orc_walker_new.argtypes = [vp, vp, i]
+    L.orc_walker_new.restype = vp
+    L.orc_walker_set.argtypes = [vp, pd, pd, vp, i]
+    L.orc_walker_next.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_int)]
+    L.orc_set_tables.argtypes = [vp, C.POINTER(abi.rt_shade), i, pd, i]
+    L.orc_add_entity.argtypes = [vp, vp, i, pd, i, i, i, i, C.POINTER(vp)]
+    L.orc_entity_in_set.argtypes = [vp, i]
+    L.orc_entity_at_pos.argtypes = [vp, vp, pd]
+    L.orc_linear_size.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.orc_linearize.argtypes = [vp, pd, pd, pi, pi, pi, pi, pi]
+    L.orc_camera_dirs.argtypes = [C.POINTER(abi.rt_camera_desc), pd]
+    L.orc_camera_scan_literal.argtypes = [C.POINTER(abi.rt_camera_desc), pi, pi, pd]
+    L.orc_trace_frame.argtypes = [vp, vp, C.POINTER(abi.rt_camera_desc), C.POINTER(abi.rt_config_desc),
+                                  i, pi, C.POINTER(C.c_float), pi, pi, pi, C.POINTER(C.c_uint8),
+                                  C.POINTER(C.c_int64), i]
+    _lib = L
+    return L
+
+
+def _vec(v):
+    return (C.c_double * 3)(*[float(x) for x in v])
+
+
+class World:
+    """An arena of reference-shaped objects (octree nodes, entities, walkers)."""
+
+    def __init__(self):
+        self.L = lib()
+        self.h = self.L.orc_world_new()
+
+    def close(self):
+        if self.h:
+            self.L.orc_world_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- octree -------------------------------------------------------------------------
+    def tree(self, pos, size, entity_set=True):
+        return self.L.orc_tree_new(self.h, _vec(pos), float(size), int(entity_set))
+
+    def new_subtree(self, t, n):
+        out = C.c_void_p()
+        r = self.L.orc_new_subtree(self.h, t, int(n), C.byref(out))
+        if r < 0:
+            raise RuntimeError("new_subtree threw")
+        return out.value
+
+    def get(self, t, n):
+        out = C.c_void_p()
+        r = self.L.orc_tree_get(t, int(n), C.byref(out))
+        if r < 0:
+            raise IndexError("Node index out of range (0..7)")
+        return out.value
+
+    def parent(self, t):
+        return self.L.orc_tree_parent(t)
+
+    def tree_id(self, t):
+        """DFS pre-order id (valid after linearize())."""
+        return self.L.orc_tree_id(t)
+
+    def dims(self, t):
+        pos = (C.c_double * 3)()
+        size = C.c_double()
+        self.L.orc_tree_dims(t, pos, C.byref(size))
+        return tuple(pos), size.value
+
+    def node_at_pos(self, t, p):
+        tree = C.c_void_p()
+        oc = C.c_int()
+        r = self.L.orc_node_at_pos(t, _vec(p), C.byref(tree), C.byref(oc))
+        if r < 0:
+            raise IndexError("Node index out of range (0..7)")
+        if r == 0:
+            return None
+        return tree.value, oc.value
+
+    # --- walker -------------------------------------------------------------------------
+    def walker(self, tree, include_undefined=False):
+        return self.L.orc_walker_new(self.h, tree, int(include_undefined))
+
+    def walk(self, wk, pos, d, node=None, limit=100000):
+        """set_pos_and_dir + each_stop(): list of (node, pos_tree, pos_octant or None)."""
+        nt, no = (node if node is not None else (None, 0))
+        if self.L.orc_walker_set(wk, _vec(pos), _vec(d), nt, int(no)) < 0:
+            raise RuntimeError("walker.set_pos_and_dir threw")
+        out = []
+        n, pt, po = C.c_void_p(), C.c_void_p(), C.c_int()
+        for _ in range(limit):
+            r = self.L.orc_walker_next(wk, C.byref(n), C.byref(pt), C.byref(po))
+            if r < 0:
+                raise RuntimeError("walker.next threw")
+            if r == 0:
+                return out
+            out.append((n.value, pt.value, None if po.value == OCT_UNDEF else po.value))
+        raise RuntimeError("walker did not terminate")
+
+    # --- scene --------------------------------------------------------------------------
+    def set_tables(self, shades, substances):
+        shades = np.ascontiguousarray(shades, dtype=abi.SHADE_DTYPE)
+        ri = np.ascontiguousarray(substances, dtype=np.float64)
+        self._shades, self._ri = shades, ri
+        self.L.orc_set_tables(self.h, shades.ctypes.data_as(C.POINTER(abi.rt_shade)), len(shades),
+                              ri.ctypes.data_as(C.POINTER(C.c_double)), len(ri))
+
+    def add_entity(self, tree, etype, geom, shade=0, substance=-1, max_in_depth=10, max_out_depth=0):
+        g = (C.c_double * 9)(*([float(x) for x in geom] + [0.0] * (9 - len(geom))))
+        fit = C.c_void_p()
+        r = self.L.orc_add_entity(self.h, tree, int(etype), g, int(shade), int(substance),
+                                  int(max_in_depth), int(max_out_depth), C.byref(fit))
+        if r < 0:
+            raise RuntimeError("add_entity_to_octree threw (%d)" % r)
+        return r, fit.value
+
+    def add_entities(self, tree, ents):
+        for e in ents:
+            self.add_entity(tree, e["type"], e["geom"], e["shade"], e["substance"],
+                            e["max_in_depth"], e["max_out_depth"])
+
+    def in_set(self, tree, eid):
+        return bool(self.L.orc_entity_in_set(tree, int(eid)))
+
+    def entity_at_pos(self, tree, p):
+        return self.L.orc_entity_at_pos(self.h, tree, _vec(p))
+
+    def linearize(self, root):
+        nn, nl = C.c_int(), C.c_int()
+        self.L.orc_linear_size(root, C.byref(nn), C.byref(nl))
+        n, m = nn.value, nl.value
+        out = dict(node_pos=np.zeros((n, 3)), node_size=np.zeros(n),
+                   node_parent=np.zeros(n, np.int32), node_child=np.zeros((n, 8), np.int32),
+                   node_ent_begin=np.zeros(n, np.int32), node_ent_count=np.zeros(n, np.int32),
+                   list_entity=np.zeros(max(m, 1), np.int32))
+        pd_, pi_ = C.POINTER(C.c_double), C.POINTER(C.c_int32)
+        self.L.orc_linearize(root, out["node_pos"].ctypes.data_as(pd_), out["node_size"].ctypes.data_as(pd_),
+                             out["node_parent"].ctypes.data_as(pi_), out["node_child"].ctypes.data_as(pi_),
+                             out["node_ent_begin"].ctypes.data_as(pi_), out["node_ent_count"].ctypes.data_as(pi_),
+                             out["list_entity"].ctypes.data_as(pi_))
+        out["list_entity"] = out["list_entity"][:m]
+        return out
+
+    # --- frame --------------------------------------------------------------------------
+    def trace_frame(self, root, cam, cfg, pixels=None, rgb=None, nthreads=1):
+        W, H = cam.width, cam.height
+        P = W * H
+        rgb = np.zeros(P * 3, np.float32) if rgb is None else rgb
+        hit_e = np.full(P, -7, np.int32)
+        hit_n = np.full(P, -7, np.int32)
+        segs = np.zeros(P, np.int32)
+        status = np.full(P, 255, np.uint8)
+        ctr = np.zeros(11, np.int64)
+        if pixels is None:
+            npix, pix = 0, None
+        else:
+            pixels = np.ascontiguousarray(pixels, dtype=np.int32)
+            npix, pix = len(pixels), pixels.ctypes.data_as(C.POINTER(C.c_int32))
+        r = self.L.orc_trace_frame(self.h, root, C.byref(cam), C.byref(cfg), npix, pix,
+                                   rgb.ctypes.data_as(C.POINTER(C.c_float)),
+                                   hit_e.ctypes.data_as(C.POINTER(C.c_int32)),
+                                   hit_n.ctypes.data_as(C.POINTER(C.c_int32)),
+                                   segs.ctypes.data_as(C.POINTER(C.c_int32)),
+                                   status.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                   ctr.ctypes.data_as(C.POINTER(C.c_int64)), int(nthreads))
+        if r not in (0, FAULT):
+            raise RuntimeError("orc_trace_frame failed %d" % r)
+        counters = dict(zip(abi.rt_stats.COUNTERS, (int(x) for x in ctr)))
+        return dict(rgb=rgb, hit_entity=hit_e, hit_node=hit_n, segments=segs, status=status,
+                    counters=counters)
+
+
+def camera_dirs(cam):
+    out = np.zeros(cam.width * cam.height * 3)
+    lib().orc_camera_dirs(C.byref(cam), out.ctypes.data_as(C.POINTER(C.c_double)))
+    return out
+
+
+def camera_scan_literal(cam):
+    n = cam.width * cam.height
+    xs, ys, d = np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n * 3)
+    lib().orc_camera_scan_literal(C.byref(cam), xs.ctypes.data_as(C.POINTER(C.c_int32)),
+                                  ys.ctypes.data_as(C.POINTER(C.c_int32)),
+                                  d.ctypes.data_as(C.POINTER(C.c_double)))
+    return xs, ys, d.reshape(-1, 3)
+
+
+def build_scene(spec):
+    """Build a rtamd.scenes.SceneSpec into a fresh World; returns (world, root)."""
+    w = World()
+    root = w.tree(spec.root_pos, spec.root_size, True)
+    w.set_tables(spec.shades, spec.substances)
+    w.add_entities(root, spec.entities)
+    return w, root

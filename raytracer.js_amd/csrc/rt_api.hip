@@ -1,0 +1,448 @@
+// rt_api.hip — the C ABI of include/rt.h: context, scene upload, frame orchestration.
+//
+// rt_trace_frame replaces the body of Raytracer.trace_frame (src/raytracer.ts:308-330): the camera
+// state and RaytracerConfig arrive as plain structs, the scene was flattened once by
+// rt_upload_scene, the kernels run on this context's GPU, and the ExposureBuffer pixels come back
+// in the caller's Float32Array.  A ray that reaches a state where the reference throws a JS Error
+// makes the call return RT_E_FAULT (outputs still written, status[] = 2 for those pixels).
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <chrono>
+#include <new>
+#include <vector>
+
+#include "rt.h"
+#include "rt_internal.h"
+#include "rt_jsnum.h"
+
+static thread_local char g_err[512] = "";
+
+int rt_set_error(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+extern "C" const char *rt_last_error(void) { return g_err; }
+extern "C" int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+#define HIP_TRY(x)                                                                                \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) return rt_set_error(RT_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes)
+    {
+        if (bytes <= cap) return RT_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (bytes == 0) return RT_OK;
+        HIP_TRY(hipMalloc(&p, bytes));
+        cap = bytes;
+        return RT_OK;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool has_scene = false;
+    bool scatter = false;            // a mirror shade with roughness > 0 is reachable
+    RtDevScene scene{};
+    DevBuf b_node_ps, b_node_child, b_node_up, b_node_ent, b_prim, b_shades, b_ent_sub, b_sub_ri;
+    DevBuf b_setup, b_fr, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
+    DevBuf b_walk;
+    static constexpr int NEV = 256;
+    hipEvent_t ev[NEV][2] = {};
+    int ev_next = 0, ev_count = 0;
+};
+
+static int use_device(rt_ctx *c)
+{
+    HIP_TRY(hipSetDevice(c->device));
+    return RT_OK;
+}
+
+extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
+{
+    if (!out) return rt_set_error(RT_E_INVALID, "rt_create: out is null");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return rt_set_error(RT_E_NODEVICE, "rt_create: no HIP device");
+    const int dev = desc ? desc->device : 0;
+    if (dev < 0 || dev >= n) return rt_set_error(RT_E_INVALID, "rt_create: device %d of %d", dev, n);
+    rt_ctx *c = new (std::nothrow) rt_ctx();
+    if (!c) return rt_set_error(RT_E_INVALID, "rt_create: out of memory");
+    c->device = dev;
+    int r = use_device(c);
+    if (r == RT_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        r = rt_set_error(RT_E_HIP, "rt_create: hipStreamCreate failed");
+    for (int i = 0; r == RT_OK && i < rt_ctx::NEV; i++)
+        if (hipEventCreate(&c->ev[i][0]) != hipSuccess || hipEventCreate(&c->ev[i][1]) != hipSuccess)
+            r = rt_set_error(RT_E_HIP, "rt_create: hipEventCreate failed");
+    if (r == RT_OK) r = c->b_setup.ensure(sizeof(RtFrameSetup));
+    if (r == RT_OK) r = c->b_counters.ensure(sizeof(unsigned long long) * CT_N);
+    if (r == RT_OK) r = c->b_fault.ensure(sizeof(int));
+    if (r != RT_OK) {
+        rt_destroy(c);
+        return r;
+    }
+    *out = c;
+    return RT_OK;
+}
+
+extern "C" void rt_destroy(rt_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf *bufs[] = {&c->b_node_ps, &c->b_node_child, &c->b_node_up, &c->b_node_ent, &c->b_prim,
+                      &c->b_shades, &c->b_ent_sub, &c->b_sub_ri, &c->b_setup, &c->b_fr, &c->b_dirs,
+                      &c->b_rgb, &c->b_hit_e, &c->b_hit_n, &c->b_status, &c->b_counters, &c->b_fault,
+                      &c->b_walk};
+    for (DevBuf *b : bufs) b->release();
+    for (int i = 0; i < rt_ctx::NEV; i++)
+        for (int k = 0; k < 2; k++)
+            if (c->ev[i][k]) (void)hipEventDestroy(c->ev[i][k]);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+template <typename T>
+static int upload(rt_ctx *c, DevBuf &b, const T *src, size_t n)
+{
+    int r = b.ensure(sizeof(T) * (n ? n : 1));
+    if (r != RT_OK) return r;
+    if (n) HIP_TRY(hipMemcpyAsync(b.p, src, sizeof(T) * n, hipMemcpyHostToDevice, c->stream));
+    return RT_OK;
+}
+
+extern "C" int rt_upload_scene(rt_ctx *c, const rt_scene_desc *s)
+{
+    if (!c || !s) return rt_set_error(RT_E_INVALID, "rt_upload_scene: null argument");
+    const int N = s->n_nodes, NL = s->n_list, NE = s->n_entities;
+    if (N < 1 || NL < 0 || NE < 0 || s->n_shades < 0 || s->n_substances < 0)
+        return rt_set_error(RT_E_INVALID, "rt_upload_scene: bad counts");
+    if (!s->node_pos || !s->node_size || !s->node_parent || !s->node_child || !s->node_ent_begin ||
+        !s->node_ent_count || (NL && !s->list_entity) || (NE && (!s->ent_type || !s->ent_geom || !s->ent_shade || !s->ent_substance)) ||
+        (s->n_shades && !s->shades) || (s->n_substances && !s->substance_ri))
+        return rt_set_error(RT_E_INVALID, "rt_upload_scene: null array");
+    if (s->node_parent[0] != -1) return rt_set_error(RT_E_INVALID, "rt_upload_scene: node 0 must be the root");
+
+    std::vector<double> ps(4 * (size_t)N);
+    std::vector<int32_t> up(2 * (size_t)N), ent(2 * (size_t)N);
+    for (int n = 0; n < N; n++) {
+        for (int i = 0; i < 3; i++) ps[4 * n + i] = s->node_pos[3 * n + i];
+        ps[4 * n + 3] = s->node_size[n];
+        const int p = s->node_parent[n];
+        if (n > 0 && (p < 0 || p >= N)) return rt_set_error(RT_E_INVALID, "rt_upload_scene: node %d parent %d", n, p);
+        for (int k = 0; k < 8; k++) {
+            const int ch = s->node_child[8 * n + k];
+            if (ch < -1 || ch >= N || ch == 0) return rt_set_error(RT_E_INVALID, "rt_upload_scene: node %d child %d", n, ch);
+            if (ch > 0 && s->node_parent[ch] != n)
+                return rt_set_error(RT_E_INVALID, "rt_upload_scene: child %d of %d has parent %d", ch, n, s->node_parent[ch]);
+        }
+        up[2 * n] = n == 0 ? -1 : p;
+        if (n == 0) {
+            up[2 * n + 1] = RT_OCT_UNDEF;
+        } else {
+            // index_within_parent (src/octree_space.ts:113-125): geometric, never cached
+            const double sc = 2 / s->node_size[p];
+            const int32_t ix = rtjs::toint32((s->node_pos[3 * n + 0] - s->node_pos[3 * p + 0]) * sc);
+            const int32_t iy = rtjs::toint32((s->node_pos[3 * n + 1] - s->node_pos[3 * p + 1]) * sc);
+            const int32_t iz = rtjs::toint32((s->node_pos[3 * n + 2] - s->node_pos[3 * p + 2]) * sc);
+            const double idx = rtjs::octant_sum(ix, iy, iz);
+            up[2 * n + 1] = (idx >= 0 && idx <= 7) ? (int)idx : RT_OCT_BAD;
+        }
+        const int b = s->node_ent_begin[n], cnt = s->node_ent_count[n];
+        if (b < 0 || cnt < 0 || (long long)b + cnt > NL)
+            return rt_set_error(RT_E_INVALID, "rt_upload_scene: node %d entity range", n);
+        ent[2 * n] = b;
+        ent[2 * n + 1] = cnt;
+    }
+    for (int e = 0; e < NE; e++) {
+        if (s->ent_type[e] < RT_ENT_SPHERE || s->ent_type[e] > RT_ENT_FACE)
+            return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d type", e);
+        if (s->ent_shade[e] < 0 || s->ent_shade[e] >= s->n_shades)
+            return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d shade", e);
+        if (s->ent_substance[e] < -1 || s->ent_substance[e] >= s->n_substances)
+            return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d substance", e);
+    }
+    bool scatter = false;
+    std::vector<RtPrim> prim((size_t)(NL ? NL : 1));
+    for (int k = 0; k < NL; k++) {
+        const int e = s->list_entity[k];
+        if (e < 0 || e >= NE) return rt_set_error(RT_E_INVALID, "rt_upload_scene: list entry %d entity %d", k, e);
+        const double *g = s->ent_geom + 9 * (size_t)e;
+        RtPrim &p = prim[k];
+        memset(&p, 0, sizeof p);
+        const int type = s->ent_type[e];
+        if (type == RT_ENT_SPHERE) {
+            p.g[0] = g[0]; p.g[1] = g[1]; p.g[2] = g[2];
+            p.g[3] = g[4];            // _dot_pp
+            p.g[4] = g[5];            // Sphere._radius_sq
+            p.g[5] = g[6];            // SphereEntity._radius_sq (is_within)
+            p.g[6] = 2 / g[3];        // 2 / diameter (normal scale)
+        } else if (type == RT_ENT_BOX) {
+            p.g[0] = g[0]; p.g[1] = g[1]; p.g[2] = g[2]; p.g[3] = g[3];
+        } else {
+            for (int i = 0; i < 3; i++) {
+                p.g[i] = g[i];
+                p.g[3 + i] = g[3 + i] - g[i];   // e1 = v1 - v0
+                p.g[6 + i] = g[6 + i] - g[i];   // e2 = v2 - v0
+            }
+        }
+        p.meta = type | (s->ent_shade[e] << 2);
+        p.entity = e;
+        const rt_shade &sh = s->shades[s->ent_shade[e]];
+        if (!sh.light && sh.response == RT_RESP_REFLECTION && sh.mirror && sh.roughness > 0.0) scatter = true;
+    }
+    int r = use_device(c);
+    if (r != RT_OK) return r;
+    c->has_scene = false;
+    if ((r = upload(c, c->b_node_ps, ps.data(), ps.size())) != RT_OK) return r;
+    if ((r = upload(c, c->b_node_child, s->node_child, 8 * (size_t)N)) != RT_OK) return r;
+    if ((r = upload(c, c->b_node_up, up.data(), up.size())) != RT_OK) return r;
+    if ((r = upload(c, c->b_node_ent, ent.data(), ent.size())) != RT_OK) return r;
+    if ((r = upload(c, c->b_prim, prim.data(), prim.size())) != RT_OK) return r;
+    if ((r = upload(c, c->b_shades, s->shades, (size_t)s->n_shades)) != RT_OK) return r;
+    if ((r = upload(c, c->b_ent_sub, s->ent_substance, (size_t)NE)) != RT_OK) return r;
+    if ((r = upload(c, c->b_sub_ri, s->substance_ri, (size_t)s->n_substances)) != RT_OK) return r;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    RtDevScene &d = c->scene;
+    d.node_ps = (const double *)c->b_node_ps.p;
+    d.node_child = (const int32_t *)c->b_node_child.p;
+    d.node_up = (const int32_t *)c->b_node_up.p;
+    d.node_ent = (const int32_t *)c->b_node_ent.p;
+    d.prim = (const RtPrim *)c->b_prim.p;
+    d.shades = (const rt_shade *)c->b_shades.p;
+    d.ent_sub = (const int32_t *)c->b_ent_sub.p;
+    d.sub_ri = (const double *)c->b_sub_ri.p;
+    d.n_nodes = N; d.n_list = NL; d.n_entities = NE; d.n_shades = s->n_shades; d.n_subs = s->n_substances;
+    c->scatter = scatter;
+    c->has_scene = true;
+    return RT_OK;
+}
+
+static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg)
+{
+    if (!c || !cam || !cfg) return rt_set_error(RT_E_INVALID, "null argument");
+    if (!c->has_scene) return rt_set_error(RT_E_NOSCENE, "no scene uploaded");
+    if (cam->width <= 0 || cam->height <= 0 || (long long)cam->width * cam->height > (1ll << 31) / 3)
+        return rt_set_error(RT_E_INVALID, "bad screen size %dx%d", cam->width, cam->height);
+    if (cfg->default_substance < -1 || cfg->default_substance >= c->scene.n_subs)
+        return rt_set_error(RT_E_INVALID, "bad default_substance %d", cfg->default_substance);
+    if (c->scatter)
+        return rt_set_error(RT_E_UNSUPPORTED,
+                            "roughness_index > 0 on a mirror: scatter_ray draws from one sequential PRNG "
+                            "(src/raytracer.ts:121-133) and is outside the GPU path");
+    return RT_OK;
+}
+
+// Prepare per-frame buffers and the launch description for one part.
+static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, int part, int n_parts,
+                   int stripe, bool want_ids, RtLaunch &L)
+{
+    const int rows = rt_part_rows(cam->height, part, n_parts, stripe);
+    const size_t P = (size_t)rows * (size_t)cam->width;
+    int r;
+    if ((r = c->b_fr.ensure(sizeof(double) * 3 * (size_t)cam->height)) != RT_OK) return r;
+    if ((r = c->b_dirs.ensure(sizeof(double) * 3 * (P ? P : 1))) != RT_OK) return r;
+    if (want_ids) {
+        if ((r = c->b_hit_e.ensure(sizeof(int32_t) * (P ? P : 1))) != RT_OK) return r;
+        if ((r = c->b_hit_n.ensure(sizeof(int32_t) * (P ? P : 1))) != RT_OK) return r;
+        if ((r = c->b_status.ensure(P ? P : 1)) != RT_OK) return r;
+    }
+    memset(&L, 0, sizeof L);
+    L.scene = c->scene;
+    L.cam = *cam;
+    L.cfg = *cfg;
+    L.part = part;
+    L.n_parts = n_parts;
+    L.stripe_rows = stripe;
+    L.rows = rows;
+    L.setup = (RtFrameSetup *)c->b_setup.p;
+    L.fr_rows = (double *)c->b_fr.p;
+    L.dirs = (double *)c->b_dirs.p;
+    L.hit_entity = want_ids ? (int32_t *)c->b_hit_e.p : nullptr;
+    L.hit_node = want_ids ? (int32_t *)c->b_hit_n.p : nullptr;
+    L.status = want_ids ? (uint8_t *)c->b_status.p : nullptr;
+    L.fault = (int32_t *)c->b_fault.p;
+    return RT_OK;
+}
+
+static void fill_stats(rt_stats *st, const unsigned long long *h)
+{
+    st->segments = (int64_t)h[CT_SEG]; st->n_ret = (int64_t)h[CT_RET]; st->n_slot = (int64_t)h[CT_SLOT];
+    st->n_loc = (int64_t)h[CT_LOC]; st->n_sph = (int64_t)h[CT_SPH]; st->n_box = (int64_t)h[CT_BOX];
+    st->n_tri = (int64_t)h[CT_TRI]; st->n_hit = (int64_t)h[CT_HIT]; st->primary = (int64_t)h[CT_PRIM];
+    st->n_warn = (int64_t)h[CT_WARN]; st->n_fault = (int64_t)h[CT_FAULT];
+}
+
+extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,
+                              int32_t *hit_entity, int32_t *hit_node, uint8_t *status, rt_stats *stats)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    int r = check_frame_args(c, cam, cfg);
+    if (r != RT_OK) return r;
+    if (!rgb_inout) return rt_set_error(RT_E_INVALID, "rt_trace_frame: rgb_inout is null");
+    if ((r = use_device(c)) != RT_OK) return r;
+    const int H = cam->height;
+    const bool ids = hit_entity || hit_node || status;
+    RtLaunch L;
+    if ((r = prepare(c, cam, cfg, 0, 1, H, ids, L)) != RT_OK) return r;
+    const size_t P = (size_t)cam->width * (size_t)H;
+    if ((r = c->b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
+    L.rgb = (float *)c->b_rgb.p;
+    L.blend = cfg->col_weight != 1.0;
+    if (L.blend) HIP_TRY(hipMemcpyAsync(L.rgb, rgb_inout, sizeof(float) * 3 * P, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->b_fault.p, 0, sizeof(int), c->stream));
+    if (stats) {
+        HIP_TRY(hipMemsetAsync(c->b_counters.p, 0, sizeof(unsigned long long) * CT_N, c->stream));
+        L.counters = (unsigned long long *)c->b_counters.p;
+    }
+    hipEvent_t *ev = c->ev[c->ev_next];
+    if ((r = rt_launch_frame(L, c->stream, ev[0], ev[1])) != RT_OK) return r;
+    HIP_TRY(hipMemcpyAsync(rgb_inout, L.rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost, c->stream));
+    if (hit_entity) HIP_TRY(hipMemcpyAsync(hit_entity, L.hit_entity, sizeof(int32_t) * P, hipMemcpyDeviceToHost, c->stream));
+    if (hit_node) HIP_TRY(hipMemcpyAsync(hit_node, L.hit_node, sizeof(int32_t) * P, hipMemcpyDeviceToHost, c->stream));
+    if (status) HIP_TRY(hipMemcpyAsync(status, L.status, P, hipMemcpyDeviceToHost, c->stream));
+    int fault = 0;
+    HIP_TRY(hipMemcpyAsync(&fault, c->b_fault.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    unsigned long long h[CT_N] = {};
+    if (stats) HIP_TRY(hipMemcpyAsync(h, c->b_counters.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (stats) {
+        memset(stats, 0, sizeof *stats);
+        fill_stats(stats, h);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+        stats->kernel_ms = ms;
+        stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    if (fault) return rt_set_error(RT_E_FAULT, "a ray reached a state where the reference throws (status 2/3 pixels)");
+    return RT_OK;
+}
+
+extern "C" int rt_trace_rows_device(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, int32_t part,
+                                    int32_t n_parts, int32_t stripe_rows, void *d_rgb, void *stream,
+                                    int32_t *rows_out, rt_stats *stats)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    int r = check_frame_args(c, cam, cfg);
+    if (r != RT_OK) return r;
+    if (n_parts < 1 || part < 0 || part >= n_parts || stripe_rows < 1)
+        return rt_set_error(RT_E_INVALID, "rt_trace_rows_device: bad partition %d/%d stripe %d", part, n_parts, stripe_rows);
+    if ((r = use_device(c)) != RT_OK) return r;
+    RtLaunch L;
+    if ((r = prepare(c, cam, cfg, part, n_parts, stripe_rows, false, L)) != RT_OK) return r;
+    if (rows_out) *rows_out = L.rows;
+    if (!d_rgb && L.rows > 0) return rt_set_error(RT_E_INVALID, "rt_trace_rows_device: d_rgb is null");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    L.rgb = (float *)d_rgb;
+    L.blend = 0;
+    if (stats) {
+        HIP_TRY(hipMemsetAsync(c->b_counters.p, 0, sizeof(unsigned long long) * CT_N, st));
+        L.counters = (unsigned long long *)c->b_counters.p;
+    }
+    hipEvent_t *ev = c->ev[c->ev_next];
+    c->ev_next = (c->ev_next + 1) % rt_ctx::NEV;
+    c->ev_count = c->ev_count < rt_ctx::NEV ? c->ev_count + 1 : rt_ctx::NEV;
+    if ((r = rt_launch_frame(L, st, ev[0], ev[1])) != RT_OK) return r;
+    if (stats) {
+        unsigned long long h[CT_N] = {};
+        HIP_TRY(hipMemcpyAsync(h, c->b_counters.p, sizeof h, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        memset(stats, 0, sizeof *stats);
+        fill_stats(stats, h);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+        stats->kernel_ms = ms;
+        stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_kernel_times(rt_ctx *c, double *ms_out, int32_t n)
+{
+    if (!c || (!ms_out && n > 0)) return rt_set_error(RT_E_INVALID, "rt_kernel_times: null argument");
+    int k = n < c->ev_count ? n : c->ev_count;
+    for (int i = 0; i < k; i++) {
+        const int idx = ((c->ev_next - k + i) % rt_ctx::NEV + rt_ctx::NEV) % rt_ctx::NEV;
+        HIP_TRY(hipEventSynchronize(c->ev[idx][1]));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[idx][0], c->ev[idx][1]));
+        ms_out[i] = ms;
+    }
+    return k;
+}
+
+extern "C" int rt_debug_walk(rt_ctx *c, const double origin[3], const double dir[3], int32_t include_undefined,
+                             int32_t max_out, int32_t *out_tree, int32_t *out_octant, int32_t *n_out)
+{
+    if (!c || !origin || !dir || !out_tree || !out_octant || !n_out || max_out < 0)
+        return rt_set_error(RT_E_INVALID, "rt_debug_walk: bad argument");
+    if (!c->has_scene) return rt_set_error(RT_E_NOSCENE, "no scene uploaded");
+    int r;
+    if ((r = use_device(c)) != RT_OK) return r;
+    if ((r = c->b_walk.ensure(sizeof(int32_t) * (2 * (size_t)max_out + 1))) != RT_OK) return r;
+    int32_t *d_tree = (int32_t *)c->b_walk.p, *d_oct = d_tree + max_out, *d_n = d_oct + max_out;
+    if ((r = rt_launch_debug_walk(c->scene, origin, dir, include_undefined, max_out, d_tree, d_oct, d_n, c->stream)) != RT_OK)
+        return r;
+    int32_t n = 0;
+    HIP_TRY(hipMemcpyAsync(&n, d_n, sizeof n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (n < 0) return rt_set_error(RT_E_FAULT, "rt_debug_walk: the walker threw");
+    HIP_TRY(hipMemcpy(out_tree, d_tree, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out_octant, d_oct, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    *n_out = n;
+    return RT_OK;
+}
+
+extern "C" int rt_debug_camera_dirs(rt_ctx *c, const rt_camera_desc *cam, double *dirs_out)
+{
+    if (!c || !cam || !dirs_out) return rt_set_error(RT_E_INVALID, "rt_debug_camera_dirs: null argument");
+    if (!c->has_scene) return rt_set_error(RT_E_NOSCENE, "no scene uploaded");
+    if (cam->width <= 0 || cam->height <= 0) return rt_set_error(RT_E_INVALID, "bad screen size");
+    int r;
+    if ((r = use_device(c)) != RT_OK) return r;
+    rt_config_desc cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.refmax = 1;
+    cfg.default_substance = -1;
+    cfg.col_weight = 1;
+    RtLaunch L;
+    if ((r = prepare(c, cam, &cfg, 0, 1, cam->height, false, L)) != RT_OK) return r;
+    const size_t P = (size_t)cam->width * (size_t)cam->height;
+    if ((r = c->b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
+    L.rgb = (float *)c->b_rgb.p;
+    L.skip_trace = 1;
+    if ((r = rt_launch_frame(L, c->stream, nullptr, nullptr)) != RT_OK) return r;
+    std::vector<double> soa(3 * P);
+    HIP_TRY(hipMemcpyAsync(soa.data(), L.dirs, sizeof(double) * 3 * P, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (size_t p = 0; p < P; p++)
+        for (int i = 0; i < 3; i++) dirs_out[3 * p + i] = soa[i * P + p];
+    return RT_OK;
+}

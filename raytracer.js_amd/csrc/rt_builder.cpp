@@ -1,0 +1,340 @@
+// rt_builder.cpp — native scene construction behind rt_builder_* (include/rt.h).
+//
+// Implements the reference's add_entity_to_octree (src/octree_entity.ts:174-188) with
+// get_covering_node_for_entity (:60-79), extend_tree_inside_to_fit_up_to_depth (:92-114),
+// extend_tree_outside_to_fit_up_to_depth (:125-171) and Entity.set_octree (src/entity.ts:50-56)
+// over an index-based node pool, then linearises the tree the way rt_upload_scene consumes it:
+// DFS pre-order from the root (children 0..7), per-node entity lists in EntitySet insertion order.
+// The JS host builds the same trees with the reference's own classes and serialises them to the
+// identical layout (raytracer.js_amd/js/serialize.js).
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "rt.h"
+#include "rt_internal.h"
+#include "rt_jsnum.h"
+
+namespace {
+
+struct BNode {
+    double pos[3];
+    double size;
+    int parent;
+    int child[8];
+    std::vector<int> set;   // EntitySet.set, insertion order
+};
+
+struct BEnt {
+    int type;
+    double g[9];
+    int shade, substance;
+    int owner;              // Entity._octree (-1 = none)
+};
+
+}  // namespace
+
+struct rt_builder {
+    std::vector<BNode> nodes;
+    std::vector<BEnt> ents;
+    int root = 0;           // the tree handed to add_entity_to_octree (the Raytracer's otree)
+    // linearised output (kept alive for rt_builder_desc)
+    std::vector<double> l_pos, l_size, l_geom;
+    std::vector<int32_t> l_parent, l_child, l_begin, l_count, l_list, l_type, l_shade, l_sub;
+    std::vector<rt_shade> l_shades;
+    std::vector<double> l_ri;
+};
+
+using namespace rtjs;
+
+static int new_node(rt_builder *b, const double pos[3], double size, int parent)
+{
+    BNode n;
+    n.pos[0] = pos[0]; n.pos[1] = pos[1]; n.pos[2] = pos[2];
+    n.size = size;
+    n.parent = parent;
+    for (int i = 0; i < 8; i++) n.child[i] = -1;
+    b->nodes.push_back(std::move(n));
+    return (int)b->nodes.size() - 1;
+}
+
+static int get_root(const rt_builder *b, int t)
+{
+    while (b->nodes[t].parent >= 0) t = b->nodes[t].parent;
+    return t;
+}
+
+static int get_level(const rt_builder *b, int t)
+{
+    int l = 0;
+    while ((t = b->nodes[t].parent) >= 0) l++;
+    return l;
+}
+
+// point_in_space(..., CLOSE_OPEN) on a cube — src/space.ts:55-66
+static bool point_in_cube(const double p[3], const double s[3], double size)
+{
+    for (int i = 0; i < 3; i++)
+        if (!(p[i] >= s[i] && p[i] < s[i] + size)) return false;
+    return true;
+}
+
+// aabb_in_space → space_in_space — src/space.ts:85-103
+static bool aabb_in_cube(const double a[3], double asize, const double s[3], double ssize)
+{
+    for (int d = 0; d < 3; d++) {
+        double ext_end = s[d] + ssize;
+        double int_end = a[d] + asize;
+        if (!(a[d] >= s[d] && int_end <= ext_end)) return false;
+    }
+    return true;
+}
+
+// node_at_pos — src/octree_space.ts:61-93.  1 found, 0 null, -1 Octree.get threw.
+static int node_at_pos(const rt_builder *b, int octree, const double p[3], int *tree_out)
+{
+    const BNode &dim = b->nodes[octree];
+    if (!point_in_cube(p, dim.pos, dim.size)) return 0;
+    int cur = get_root(b, octree);
+    double np[3] = {dim.pos[0], dim.pos[1], dim.pos[2]};
+    double ns = dim.size;
+    int next = cur;
+    while (next >= 0) {
+        double s = 2 / ns;
+        int32_t ix = toint32((p[0] - np[0]) * s);
+        int32_t iy = toint32((p[1] - np[1]) * s);
+        int32_t iz = toint32((p[2] - np[2]) * s);
+        cur = next;
+        double idx = octant_sum(ix, iy, iz);
+        if (!(idx >= 0 && idx <= 7)) return -1;
+        next = b->nodes[cur].child[(int)idx];
+        ns /= 2;
+        np[0] += (double)ix * ns;
+        np[1] += (double)iy * ns;
+        np[2] += (double)iz * ns;
+    }
+    *tree_out = cur;
+    return 1;
+}
+
+// Entity.get_aabb (sphere src/entities/entity_sphere.ts:90-96, box src/entities/entity_box.ts:75-82,
+// face: min corner + max extent)
+static void entity_aabb(const BEnt &e, double a[3], double *asize)
+{
+    const double *g = e.g;
+    if (e.type == RT_ENT_SPHERE) {
+        double d = g[3];
+        for (int i = 0; i < 3; i++) a[i] = g[i] - d * 0.5;
+        *asize = d;
+    } else if (e.type == RT_ENT_BOX) {
+        double h = g[3] / 2;
+        for (int i = 0; i < 3; i++) a[i] = g[i] - h;
+        *asize = g[3];
+    } else {
+        double ext[3];
+        for (int i = 0; i < 3; i++) {
+            double mn = jmin(jmin(g[i], g[3 + i]), g[6 + i]);
+            double mx = jmax(jmax(g[i], g[3 + i]), g[6 + i]);
+            a[i] = mn;
+            ext[i] = mx - mn;
+        }
+        *asize = jmax(jmax(ext[0], ext[1]), ext[2]);
+    }
+}
+
+static int extend_inside(rt_builder *b, int root, int node, const double a[3], double asize, int max_depth)
+{
+    int cur_depth = get_level(b, node) - get_level(b, root);
+    int cur = node;
+    while (cur_depth < max_depth) {
+        const double cs = b->nodes[cur].size;
+        double s = 2.0 / cs;
+        int32_t xyz[3];
+        double half = cs / 2;
+        double sp[3];
+        for (int i = 0; i < 3; i++) xyz[i] = toint32((a[i] - b->nodes[cur].pos[i]) * s);
+        for (int i = 0; i < 3; i++) sp[i] = b->nodes[cur].pos[i] + (double)xyz[i] * half;
+        if (!aabb_in_cube(a, asize, sp, half)) break;
+        int idx = (int)(((uint32_t)xyz[2] << 2) | ((uint32_t)xyz[1] << 1) | ((uint32_t)xyz[0] << 0));
+        if (!(idx >= 0 && idx <= 7)) return -1;
+        int nt = new_node(b, sp, cs / 2, cur);
+        b->nodes[cur].child[idx] = nt;          // replaces an existing child, exactly like Octree.set
+        cur = nt;
+        cur_depth++;
+    }
+    return cur;
+}
+
+static int extend_outside(rt_builder *b, int root, int node, const double a[3], double asize, int max_depth)
+{
+    if (b->nodes[node].parent >= 0) return -1;
+    int cur_depth = get_level(b, root) - get_level(b, node);
+    int cur = node;
+    while (cur_depth < max_depth) {
+        const double cs = b->nodes[cur].size;
+        double s = 1.0 / cs;
+        double al[3], pp[3];
+        for (int i = 0; i < 3; i++) {
+            al[i] = (a[i] - b->nodes[cur].pos[i]) * s;
+            al[i] = jmax(jmin(floor(al[i]), 0), -1);
+        }
+        for (int i = 0; i < 3; i++) pp[i] = b->nodes[cur].pos[i] + al[i] * cs;
+        double psize = cs * 2;
+        int idx = (toint32(-al[2]) << 2) | (toint32(-al[1]) << 1) | (toint32(-al[0]) << 0);
+        if (!(idx >= 0 && idx <= 7)) return -1;
+        int np = new_node(b, pp, psize, -1);
+        b->nodes[np].child[idx] = cur;
+        b->nodes[cur].parent = np;
+        cur = np;
+        if (aabb_in_cube(a, asize, pp, psize)) return cur;
+        cur_depth++;
+    }
+    return -1;
+}
+
+extern "C" int rt_builder_create(const double root_pos[3], double root_size, rt_builder **out)
+{
+    if (!root_pos || !out) return rt_set_error(RT_E_INVALID, "rt_builder_create: null argument");
+    rt_builder *b = new (std::nothrow) rt_builder();
+    if (!b) return rt_set_error(RT_E_INVALID, "rt_builder_create: out of memory");
+    b->root = new_node(b, root_pos, root_size, -1);
+    *out = b;
+    return RT_OK;
+}
+
+extern "C" void rt_builder_destroy(rt_builder *b) { delete b; }
+
+extern "C" int rt_builder_add(rt_builder *b, const rt_entity_in *in, int32_t *entity_id)
+{
+    if (!b || !in) return rt_set_error(RT_E_INVALID, "rt_builder_add: null argument");
+    if (in->type < RT_ENT_SPHERE || in->type > RT_ENT_FACE)
+        return rt_set_error(RT_E_INVALID, "rt_builder_add: bad entity type %d", in->type);
+    BEnt e;
+    e.type = in->type;
+    for (int i = 0; i < 9; i++) e.g[i] = in->geom[i];
+    if (e.type == RT_ENT_SPHERE) {
+        // SphereEntity ctor (src/entities/entity_sphere.ts:34-39) + Sphere.update_cache
+        // (src/math/intersection.ts:94-97)
+        double d = in->geom[3];
+        double radius = d / 2;
+        e.g[4] = dot3(in->geom[0], in->geom[1], in->geom[2], in->geom[0], in->geom[1], in->geom[2]);
+        e.g[5] = radius * radius;
+        e.g[6] = d * d / 4;
+        e.g[7] = 0;
+        e.g[8] = 0;
+    }
+    e.shade = in->shade;
+    e.substance = in->substance;
+    e.owner = -1;
+
+    double a[3], asize;
+    entity_aabb(e, a, &asize);
+    // get_covering_node_for_entity
+    int fit = -1, deepest;
+    int r = node_at_pos(b, b->root, a, &deepest);
+    if (r < 0) return rt_set_error(RT_E_TREE, "add_entity_to_octree: Node index out of range (0..7)");
+    if (r == 1) {
+        int cur = deepest;
+        do {
+            if (aabb_in_cube(a, asize, b->nodes[cur].pos, b->nodes[cur].size)) break;
+            cur = b->nodes[cur].parent;
+        } while (cur >= 0);
+        fit = cur;
+    }
+    if (fit < 0) {
+        fit = extend_outside(b, b->root, get_root(b, b->root), a, asize, in->max_out_depth);
+        if (fit < 0) return rt_set_error(RT_E_TREE, "TreeOutsideGrowError: The tree outside-depth limit exceeded");
+    }
+    fit = extend_inside(b, b->root, fit, a, asize, in->max_in_depth);
+    if (fit < 0) return rt_set_error(RT_E_TREE, "add_entity_to_octree: Node index out of range (0..7)");
+    int id = (int)b->ents.size();
+    e.owner = fit;
+    b->ents.push_back(e);
+    b->nodes[fit].set.push_back(id);   // a fresh entity: Set.add appends
+    if (entity_id) *entity_id = id;
+    return RT_OK;
+}
+
+extern "C" int rt_builder_add_many(rt_builder *b, const rt_entity_in *in, int32_t n)
+{
+    for (int32_t i = 0; i < n; i++) {
+        int r = rt_builder_add(b, in + i, nullptr);
+        if (r != RT_OK) return r;
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_builder_desc(rt_builder *b, const rt_shade *shades, int32_t n_shades,
+                               const double *substance_ri, int32_t n_substances, rt_scene_desc *out)
+{
+    if (!b || !out) return rt_set_error(RT_E_INVALID, "rt_builder_desc: null argument");
+    if (b->nodes[b->root].parent >= 0)
+        return rt_set_error(RT_E_UNSUPPORTED,
+                            "rt_builder_desc: the octree grew outward above the Raytracer's root");
+    // DFS pre-order numbering with an explicit stack (children 0..7)
+    std::vector<int> order;
+    std::vector<int> id_of(b->nodes.size(), -1);
+    std::vector<int> stack{b->root};
+    while (!stack.empty()) {
+        int t = stack.back();
+        stack.pop_back();
+        id_of[t] = (int)order.size();
+        order.push_back(t);
+        for (int c = 7; c >= 0; c--)
+            if (b->nodes[t].child[c] >= 0) stack.push_back(b->nodes[t].child[c]);
+    }
+    const size_t n = order.size();
+    b->l_pos.assign(3 * n, 0);
+    b->l_size.assign(n, 0);
+    b->l_parent.assign(n, -1);
+    b->l_child.assign(8 * n, -1);
+    b->l_begin.assign(n, 0);
+    b->l_count.assign(n, 0);
+    b->l_list.clear();
+    for (size_t k = 0; k < n; k++) {
+        const BNode &nd = b->nodes[order[k]];
+        for (int i = 0; i < 3; i++) b->l_pos[3 * k + i] = nd.pos[i];
+        b->l_size[k] = nd.size;
+        b->l_parent[k] = nd.parent >= 0 && order[k] != b->root ? id_of[nd.parent] : -1;
+        for (int c = 0; c < 8; c++) b->l_child[8 * k + c] = nd.child[c] >= 0 ? id_of[nd.child[c]] : -1;
+        b->l_begin[k] = (int32_t)b->l_list.size();
+        b->l_count[k] = (int32_t)nd.set.size();
+        for (int e : nd.set) b->l_list.push_back(e);
+    }
+    const size_t ne = b->ents.size();
+    b->l_type.resize(ne);
+    b->l_shade.resize(ne);
+    b->l_sub.resize(ne);
+    b->l_geom.resize(9 * ne);
+    for (size_t i = 0; i < ne; i++) {
+        b->l_type[i] = b->ents[i].type;
+        b->l_shade[i] = b->ents[i].shade;
+        b->l_sub[i] = b->ents[i].substance;
+        memcpy(&b->l_geom[9 * i], b->ents[i].g, 9 * sizeof(double));
+    }
+    b->l_shades.assign(shades, shades + (n_shades > 0 ? n_shades : 0));
+    b->l_ri.assign(substance_ri, substance_ri + (n_substances > 0 ? n_substances : 0));
+    memset(out, 0, sizeof(*out));
+    out->n_nodes = (int32_t)n;
+    out->n_list = (int32_t)b->l_list.size();
+    out->n_entities = (int32_t)ne;
+    out->n_shades = n_shades;
+    out->n_substances = n_substances;
+    out->node_pos = b->l_pos.data();
+    out->node_size = b->l_size.data();
+    out->node_parent = b->l_parent.data();
+    out->node_child = b->l_child.data();
+    out->node_ent_begin = b->l_begin.data();
+    out->node_ent_count = b->l_count.data();
+    out->list_entity = b->l_list.data();
+    out->ent_type = b->l_type.data();
+    out->ent_geom = b->l_geom.data();
+    out->ent_shade = b->l_shade.data();
+    out->ent_substance = b->l_sub.data();
+    out->shades = b->l_shades.data();
+    out->substance_ri = b->l_ri.data();
+    return RT_OK;
+}

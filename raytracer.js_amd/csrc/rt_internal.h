@@ -1,0 +1,84 @@
+// rt_internal.h — shared between the C-ABI host code (rt_api.hip, rt_builder.cpp) and the kernels.
+#pragma once
+
+#include <stdint.h>
+
+#include "rt.h"
+
+// Error reporting: thread-local message behind rt_last_error().
+int rt_set_error(int code, const char *fmt, ...);
+
+// ---- device scene layout (HBM) ---------------------------------------------------------------
+// Node records are split by access pattern (SoA of small records):
+//   node_ps   double4  {pos.x, pos.y, pos.z, size}       read by update_next_pos / step_in
+//   node_child int32[8]                                  read on every walker slot visit
+//   node_up   int2     {parent, index_within_parent}     read by step_back
+//   node_ent  int2     {list begin, count}               read when a node is returned
+// Primitives are re-packed in list order (each entity appears in exactly one EntitySet), so a
+// node's entity scan streams one contiguous run of 80-byte records.
+enum : int { RT_OCT_UNDEF = -1, RT_OCT_BAD = 1000 };
+
+struct alignas(16) RtPrim {
+    double g[9];       // SPHERE: pos.xyz, dot_pp, radius_sq, within_rsq, 2/diameter
+                       // BOX:    pos.xyz, size
+                       // FACE:   v0.xyz, e1.xyz, e2.xyz
+    int32_t meta;      // type | shade << 2
+    int32_t entity;    // entity id (creation order)
+};
+static_assert(sizeof(RtPrim) == 80, "RtPrim must stay 80 bytes");
+
+struct RtDevScene {
+    const double *node_ps;      // [n_nodes*4]
+    const int32_t *node_child;  // [n_nodes*8]
+    const int32_t *node_up;     // [n_nodes*2]
+    const int32_t *node_ent;    // [n_nodes*2]
+    const RtPrim *prim;         // [n_list]
+    const rt_shade *shades;     // [n_shades]
+    const int32_t *ent_sub;     // [n_entities]
+    const double *sub_ri;       // [n_substances]
+    int32_t n_nodes, n_list, n_entities, n_shades, n_subs, pad_;
+};
+
+// Per-frame state computed on the device by the setup kernel.
+struct RtFrameSetup {
+    int32_t start_tree;   // node_at_pos(otree, camera.pos) → tree (-1: null)
+    int32_t start_oct;
+    int32_t start_sub;    // start substance (-1: undefined)
+    int32_t fault;
+};
+
+// Counter slots (rt_stats order).
+enum { CT_SEG, CT_RET, CT_SLOT, CT_LOC, CT_SPH, CT_BOX, CT_TRI, CT_HIT, CT_PRIM, CT_WARN, CT_FAULT, CT_N };
+
+// Kernel launchers (rt_kernels.hip).
+struct RtLaunch {
+    RtDevScene scene;
+    rt_camera_desc cam;
+    rt_config_desc cfg;
+    int32_t part, n_parts, stripe_rows, rows;   // this part's row set
+    RtFrameSetup *setup;                        // device
+    double *fr_rows;                            // device [H*3]
+    double *dirs;                               // device [3][rows*W] (SoA planes)
+    float *rgb;                                 // device [rows*W*3]
+    int32_t *hit_entity, *hit_node;             // device [rows*W] or null
+    uint8_t *status;                            // device [rows*W] or null
+    unsigned long long *counters;               // device [CT_N] or null (stats build)
+    int32_t *fault;                             // device flag: some ray hit a reference throw
+    int32_t blend;                              // col_weight != 1: read-modify-write rgb
+    int32_t skip_trace;                         // ray generation only (rt_debug_camera_dirs)
+};
+
+int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end);
+int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[3], int include_undefined,
+                         int max_out, int32_t *d_tree, int32_t *d_oct, int32_t *d_n, void *stream);
+
+// Row bookkeeping for the stripe partition.
+static inline int32_t rt_part_rows(int32_t H, int32_t part, int32_t n_parts, int32_t stripe)
+{
+    int32_t n_stripes = (H + stripe - 1) / stripe, rows = 0;
+    for (int32_t s = part; s < n_stripes; s += n_parts) {
+        int32_t r0 = s * stripe, r1 = r0 + stripe < H ? r0 + stripe : H;
+        rows += r1 - r0;
+    }
+    return rows;
+}

@@ -1,0 +1,666 @@
+// rt_kernels.hip — gfx950 kernels of the raytracer.js render path.
+//
+//   k_frame_setup   once per frame: start node / start substance (src/raytracer.ts:309-313) and the
+//                   vertical scan chains of Camera.get_dir_for_each_pixel (src/view/camera.ts:231-249)
+//   k_raygen        one lane per half-row: the horizontal scan chains (src/view/camera.ts:215-229)
+//   k_trace         one lane per pixel: Ray.trace (src/raytracer.ts:168-277) over the linearised
+//                   octree with the OctreeWalker visit order (src/octree_space.ts:316-361), entity
+//                   tests (src/entities/*), SolidMaterial shading, sky / inverse-square law, and the
+//                   ExposureBuffer blend + f32 store (src/view/exposure_buffer.ts:77-91)
+//   k_debug_walk    one lane: the walker's stop sequence (KAT checks)
+//
+// Numerics: binary64 with the reference's operation order, IEEE division and sqrt, no contraction
+// (built with -ffp-contract=off), JS ToInt32 for `<<`.  Branchy pointer-chasing work: no MFMA.
+#include <hip/hip_runtime.h>
+
+#include "rt_internal.h"
+#include "rt_jsnum.h"
+
+using namespace rtjs;
+
+namespace {
+
+constexpr int ST_OK = 0, ST_WARN = 1, ST_FAULT = 2, ST_CAP = 3;
+constexpr long long STEP_CAP = 1ll << 24;        // per-ray loop bound: every lane terminates
+
+// ---- node access --------------------------------------------------------------------------------
+struct NodeDims { double x, y, z, s; };
+
+__device__ __forceinline__ NodeDims node_dims(const RtDevScene &S, int n)
+{
+    const double4 v = reinterpret_cast<const double4 *>(S.node_ps)[n];
+    return {v.x, v.y, v.z, v.w};
+}
+
+// ---- Box.line_intersection (src/math/intersection.ts:150-204) on a cube ----------------------------
+// Returns false for [] (u1 > u2).  i1/i2 = -1 when the face index stayed undefined.
+struct BoxIsect { double u1, u2; int i1, i2; };
+
+__device__ __forceinline__ bool box_isect(double cx, double cy, double cz, double size,
+                                          const double o[3], const double d[3], BoxIsect &r)
+{
+    const double hs = size * 0.5;
+    const double c[3] = {cx, cy, cz};
+    double u1 = -INFINITY, u2 = INFINITY;
+    int i1 = -1, i2 = -1;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double tl = c[a] - hs;
+        const double qlo = o[a] - tl;
+        const double qhi = tl + size - o[a];
+        // face 2a: p = -d[a], q = qlo ; face 2a+1: p = d[a], q = qhi  (loop order of the reference)
+        const double plo = -d[a], phi = d[a];
+        const double ulo = qlo / plo;
+        if (is_negative(plo)) { if (ulo > u1) { u1 = ulo; i1 = 2 * a; } }
+        else                  { if (ulo < u2) { u2 = ulo; i2 = 2 * a; } }
+        const double uhi = qhi / phi;
+        if (is_negative(phi)) { if (uhi > u1) { u1 = uhi; i1 = 2 * a + 1; } }
+        else                  { if (uhi < u2) { u2 = uhi; i2 = 2 * a + 1; } }
+    }
+    if (u1 > u2) return false;
+    r.u1 = u1; r.u2 = u2; r.i1 = i1; r.i2 = i2;
+    return true;
+}
+
+// FACE_NORMALS[i] (src/math/intersection.ts:141-148) component `axis`
+__device__ __forceinline__ double face_normal(int i, int axis)
+{
+    return (i >> 1) == axis ? ((i & 1) ? 1.0 : -1.0) : 0.0;
+}
+
+// ---- point location -------------------------------------------------------------------------------
+__device__ __forceinline__ bool point_in_cube(const double p[3], double x, double y, double z, double s)
+{
+    return (p[0] >= x && p[0] < x + s) && (p[1] >= y && p[1] < y + s) && (p[2] >= z && p[2] < z + s);
+}
+
+// node_at_pos(root, p) — src/octree_space.ts:61-93.  1 found, 0 null, -1 Octree.get threw.
+__device__ int node_at_pos(const RtDevScene &S, const double p[3], int &tree, int &oct, long long &levels)
+{
+    const NodeDims r = node_dims(S, 0);
+    if (!point_in_cube(p, r.x, r.y, r.z, r.s)) return 0;
+    double np0 = r.x, np1 = r.y, np2 = r.z, ns = r.s;
+    int cur = 0, next = 0, idx = 0;
+    while (next >= 0) {
+        levels++;
+        const double s = 2 / ns;
+        const int32_t ix = toint32((p[0] - np0) * s);
+        const int32_t iy = toint32((p[1] - np1) * s);
+        const int32_t iz = toint32((p[2] - np2) * s);
+        cur = next;
+        const double di = octant_sum(ix, iy, iz);
+        if (!(di >= 0 && di <= 7)) return -1;
+        idx = (int)di;
+        next = S.node_child[8 * cur + idx];
+        ns /= 2;
+        np0 += (double)ix * ns;
+        np1 += (double)iy * ns;
+        np2 += (double)iz * ns;
+    }
+    tree = cur;
+    oct = idx;
+    return 1;
+}
+
+// ---- OctreeWalker (src/octree_space.ts:159-408) ---------------------------------------------------
+enum : int { F_RET = 1, F_STEPPED = 2, F_AHEAD = 4 };
+
+struct Walker {
+    double o[3], d[3];     // this.pos / this.direction
+    double np[3];          // next_pos[0]
+    int nn;                // next_pos[1]: face index | negate << 3 | valid << 4
+    int cur_tree;          // -1: cur_node undefined
+    int cur_oct;           // RT_OCT_UNDEF, 0..7, or RT_OCT_BAD
+    int depth;
+    int flags;
+};
+
+struct Counters {
+    long long ret, slot, loc, sph, box, tri, hit, steps;
+};
+
+// setup_cur_node — :251-278.  Returns 1/0 or -1 (throw).
+__device__ int walker_setup(const RtDevScene &S, Walker &w)
+{
+    w.np[0] = w.o[0]; w.np[1] = w.o[1]; w.np[2] = w.o[2];
+    w.nn = 0;
+    w.flags = 0;
+    w.depth = 0;
+    if (w.cur_tree >= 0) return 1;
+    const NodeDims r = node_dims(S, 0);
+    BoxIsect bi;
+    if (!box_isect(r.x + 0.5 * r.s, r.y + 0.5 * r.s, r.z + 0.5 * r.s, 1 * r.s, w.o, w.d, bi)) return 0;
+    double t;
+    int fi;
+    if (bi.u1 >= 0) { t = bi.u1; fi = bi.i1; }
+    else if (bi.u2 >= 0) { t = bi.u2; fi = bi.i2; }
+    else return 0;
+    const double ip0 = w.o[0] + w.d[0] * t, ip1 = w.o[1] + w.d[1] * t, ip2 = w.o[2] + w.d[2] * t;
+    if (fi < 0) return -1;                                   // vector.negate(undefined)
+    w.cur_tree = 0;
+    w.cur_oct = RT_OCT_UNDEF;
+    w.np[0] = ip0; w.np[1] = ip1; w.np[2] = ip2;
+    w.nn = fi | 8 | 16;
+    return 1;
+}
+
+// set_pos_and_dir(pos, dir, node?) — :188-226.  Returns 0 or -1 (throw).
+__device__ int walker_set(const RtDevScene &S, Walker &w, const double o[3], const double d[3],
+                          bool have_node, int tree, int oct, Counters &c)
+{
+    w.d[0] = d[0]; w.d[1] = d[1]; w.d[2] = d[2];
+    if (have_node) {
+        w.cur_tree = tree;
+        w.cur_oct = oct;
+    } else {
+        int t = -1, oc = 0;
+        const int r = node_at_pos(S, o, t, oc, c.loc);
+        if (r < 0) return -1;
+        if (r == 1) { w.cur_tree = t; w.cur_oct = oc; }
+        else { w.cur_tree = -1; w.cur_oct = RT_OCT_UNDEF; }
+    }
+    w.o[0] = o[0]; w.o[1] = o[1]; w.o[2] = o[2];
+    return walker_setup(S, w) < 0 ? -1 : 0;
+}
+
+// update_next_pos — :369-384 with dim_relative_to_parent :127-136.  Returns 0 or -1 (throw).
+__device__ __forceinline__ int walker_update_next_pos(const RtDevScene &S, Walker &w, Counters &c)
+{
+    c.slot++;
+    const NodeDims p = node_dims(S, w.cur_tree);
+    const int n = w.cur_oct;
+    const double ph = p.s / 2;
+    const double dx = p.x + (double)((n >> 0) & 1) * ph;
+    const double dy = p.y + (double)((n >> 1) & 1) * ph;
+    const double dz = p.z + (double)((n >> 2) & 1) * ph;
+    BoxIsect bi;
+    if (!box_isect(dx + 0.5 * ph, dy + 0.5 * ph, dz + 0.5 * ph, 1 * ph, w.o, w.d, bi)) return -1;
+    w.np[0] = w.o[0] + w.d[0] * bi.u2;
+    w.np[1] = w.o[1] + w.d[1] * bi.u2;
+    w.np[2] = w.o[2] + w.d[2] * bi.u2;
+    w.nn = bi.i2 >= 0 ? (bi.i2 | 16) : 0;
+    return 0;
+}
+
+// next — :316-361.  Returns 1 with (node, slot tree, slot octant), 0 at the end, -1 on a throw,
+// -2 at the step cap.
+template <bool INCL_UNDEF>
+__device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_tree, int &pos_oct, Counters &c)
+{
+    while (w.cur_tree >= 0) {
+        if (++c.steps > STEP_CAP) return -2;
+        const int ltree = w.cur_tree, loct = w.cur_oct;
+        int lnode;
+        if (loct != RT_OCT_UNDEF) {
+            if ((unsigned)loct > 7u) return -1;              // Octree.get: index out of range
+            lnode = S.node_child[8 * ltree + loct];
+        } else {
+            lnode = ltree;
+        }
+        if (!(w.flags & F_RET)) {
+            if (INCL_UNDEF || lnode >= 0) {
+                w.flags |= F_RET;
+                node = lnode; pos_tree = ltree; pos_oct = loct;
+                c.ret++;
+                return 1;
+            }
+        }
+        if (loct != RT_OCT_UNDEF) {
+            if (!(w.flags & F_AHEAD)) {
+                if (!(w.flags & F_STEPPED) && lnode >= 0) {
+                    // octant_adj_pos(node, next_pos[0]) — :41-50, then step_in — :310-314
+                    const NodeDims cd = node_dims(S, lnode);
+                    const double h = cd.s / 2;
+                    const int px = w.np[0] >= cd.x + h, py = w.np[1] >= cd.y + h, pz = w.np[2] >= cd.z + h;
+                    w.depth++;
+                    w.cur_tree = lnode;
+                    w.cur_oct = (pz << 2) | (py << 1) | px;
+                    w.flags &= ~F_RET;
+                    continue;
+                }
+                if (walker_update_next_pos(S, w, c) < 0) return -1;
+            }
+            if (!(w.nn & 16)) return -1;                     // vector.add(v, undefined)
+            // cur_octant + normal: only the normal's axis can leave {0,1}
+            const int face = w.nn & 7, axis = face >> 1;
+            int delta = (face & 1) ? 1 : -1;
+            if (w.nn & 8) delta = -delta;
+            const int nb = ((loct >> axis) & 1) + delta;
+            if (nb >= 0 && nb <= 1) {
+                w.cur_oct = (loct & ~(1 << axis)) | (nb << axis);
+                w.flags = 0;
+                continue;
+            }
+            w.flags |= F_AHEAD;
+        }
+        // step_back — :280-308
+        w.flags |= F_STEPPED;
+        if (w.cur_oct == RT_OCT_UNDEF) {
+            w.cur_tree = -1;
+            w.flags &= ~F_RET;
+        } else {
+            if (w.depth > 0) { w.depth--; w.flags |= F_RET; }
+            else w.flags &= ~F_RET;
+            const int2 up = reinterpret_cast<const int2 *>(S.node_up)[w.cur_tree];
+            if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
+            else w.cur_oct = RT_OCT_UNDEF;
+        }
+    }
+    return 0;
+}
+
+// ---- entity tests -----------------------------------------------------------------------------------
+struct Hit {
+    double p[3];
+    double n[3];
+};
+
+// SphereEntity.collision_info — src/entities/entity_sphere.ts:68-88 / Sphere.line_intersection
+// src/math/intersection.ts:109-128
+__device__ __forceinline__ bool sphere_hit(const double *g, const double o[3], const double d[3], Hit &h)
+{
+    const double dist0 = o[0] - g[0], dist1 = o[1] - g[1], dist2 = o[2] - g[2];
+    const double a = dot3(d[0], d[1], d[2], d[0], d[1], d[2]);
+    const double b = dot3(dist0, dist1, dist2, d[0], d[1], d[2]) * 2;
+    const double c = dot3(o[0], o[1], o[2], o[0], o[1], o[2]) + g[3] -
+                     dot3(o[0], o[1], o[2], g[0], g[1], g[2]) * 2 - g[4];
+    const double delta = b * b - a * c * 4;
+    if (delta < 0) return false;
+    const double s = sqrt(delta);
+    const double tmp1 = -b / (a * 2);
+    const double tmp2 = s / (a * 2);
+    const double t1 = tmp1 - tmp2, t2 = tmp1 + tmp2;
+    double t;
+    if (t1 >= 0) t = t1;
+    else if (t2 >= 0) t = t2;
+    else return false;
+    for (int i = 0; i < 3; i++) h.p[i] = o[i] + d[i] * t;
+    const double k = g[6];                                   // 2 / diameter
+    for (int i = 0; i < 3; i++) h.n[i] = (h.p[i] - g[i]) * k;
+    const double sg = -sign(dot3(d[0], d[1], d[2], h.n[0], h.n[1], h.n[2]));
+    for (int i = 0; i < 3; i++) h.n[i] *= sg;
+    return true;
+}
+
+// BoxEntity.collision_info — src/entities/entity_box.ts:54-73.  Returns 0 miss, 1 hit, -1 throw.
+__device__ __forceinline__ int box_hit(const double *g, const double o[3], const double d[3], Hit &h)
+{
+    const double size = 1 * g[3];
+    BoxIsect bi;
+    if (!box_isect(g[0], g[1], g[2], size, o, d, bi)) return 0;
+    double t;
+    int fi;
+    if (bi.u1 >= 0) { t = bi.u1; fi = bi.i1; }
+    else if (bi.u2 >= 0) { t = bi.u2; fi = bi.i2; }
+    else return 0;
+    for (int i = 0; i < 3; i++) h.p[i] = o[i] + d[i] * t;
+    if (fi < 0) return -1;                                   // vector.dot(dir, undefined)
+    const double N0 = face_normal(fi, 0), N1 = face_normal(fi, 1), N2 = face_normal(fi, 2);
+    const double sg = -sign(dot3(d[0], d[1], d[2], N0, N1, N2));
+    h.n[0] = N0 * sg; h.n[1] = N1 * sg; h.n[2] = N2 * sg;
+    return 1;
+}
+
+// FaceEntity.collision_info — DESIGN.md §Triangle (fixed-order f64 Moller-Trumbore on v0, e1, e2)
+__device__ __forceinline__ void cross3(double a0, double a1, double a2, double b0, double b1, double b2,
+                                       double &r0, double &r1, double &r2)
+{
+    r0 = a1 * b2 - a2 * b1;
+    r1 = a2 * b0 - a0 * b2;
+    r2 = a0 * b1 - a1 * b0;
+}
+
+__device__ __forceinline__ bool face_hit(const double *g, const double o[3], const double d[3], Hit &h)
+{
+    const double e10 = g[3], e11 = g[4], e12 = g[5], e20 = g[6], e21 = g[7], e22 = g[8];
+    double pv0, pv1, pv2;
+    cross3(d[0], d[1], d[2], e20, e21, e22, pv0, pv1, pv2);
+    const double det = dot3(e10, e11, e12, pv0, pv1, pv2);
+    if (!(det != 0)) return false;
+    const double inv = 1 / det;
+    const double tv0 = o[0] - g[0], tv1 = o[1] - g[1], tv2 = o[2] - g[2];
+    const double u = dot3(tv0, tv1, tv2, pv0, pv1, pv2) * inv;
+    if (!(u >= 0 && u <= 1)) return false;
+    double qv0, qv1, qv2;
+    cross3(tv0, tv1, tv2, e10, e11, e12, qv0, qv1, qv2);
+    const double v = dot3(d[0], d[1], d[2], qv0, qv1, qv2) * inv;
+    if (!(v >= 0 && u + v <= 1)) return false;
+    const double t = dot3(e20, e21, e22, qv0, qv1, qv2) * inv;
+    if (!(t >= 0)) return false;
+    for (int i = 0; i < 3; i++) h.p[i] = o[i] + d[i] * t;
+    double n0, n1, n2;
+    cross3(e10, e11, e12, e20, e21, e22, n0, n1, n2);
+    const double il = 1.0 / sqrt(dot3(n0, n1, n2, n0, n1, n2));
+    n0 = n0 * il; n1 = n1 * il; n2 = n2 * il;
+    const double sg = -sign(dot3(d[0], d[1], d[2], n0, n1, n2));
+    h.n[0] = n0 * sg; h.n[1] = n1 * sg; h.n[2] = n2 * sg;
+    return true;
+}
+
+// is_within: sphere src/entities/entity_sphere.ts:63-66, box (pos as min corner)
+// src/entities/entity_box.ts:47-52, face false.
+__device__ __forceinline__ bool prim_within(const RtPrim &pr, const double p[3])
+{
+    const int type = pr.meta & 3;
+    if (type == RT_ENT_SPHERE) {
+        const double a = p[0] - pr.g[0], b = p[1] - pr.g[1], c = p[2] - pr.g[2];
+        return dot3(a, b, c, a, b, c) <= pr.g[5];
+    }
+    if (type == RT_ENT_BOX) return point_in_cube(p, pr.g[0], pr.g[1], pr.g[2], 1 * pr.g[3]);
+    return false;
+}
+
+// entity_at_pos — src/octree_entity.ts:191-202.  Returns entity id, -1 undefined, -2 throw.
+__device__ int entity_at_pos(const RtDevScene &S, const double p[3], long long &levels)
+{
+    int t = -1, oc = 0;
+    const int r = node_at_pos(S, p, t, oc, levels);
+    if (r < 0) return -2;
+    int cur = r == 1 ? t : -1;
+    while (cur >= 0) {
+        const int2 ent = reinterpret_cast<const int2 *>(S.node_ent)[cur];
+        for (int k = ent.x; k < ent.x + ent.y; k++)
+            if (prim_within(S.prim[k], p)) return S.prim[k].entity;
+        cur = reinterpret_cast<const int2 *>(S.node_up)[cur].x;
+    }
+    return -1;
+}
+
+// ---- camera scan (src/view/camera.ts:207-250; vector.rotate_vectors src/math/vector.ts:318-323) ----
+__device__ __forceinline__ void rotate_pair(double bx[3], double by[3], double c, double s)
+{
+    double nx[3], ny[3];
+    for (int i = 0; i < 3; i++) {
+        nx[i] = bx[i] * c + by[i] * s;
+        ny[i] = bx[i] * -s + by[i] * c;
+    }
+    for (int i = 0; i < 3; i++) { bx[i] = nx[i]; by[i] = ny[i]; }
+}
+
+__device__ __forceinline__ int part_row_to_y(int lr, int part, int n_parts, int stripe)
+{
+    const int k = lr / stripe;
+    return (part + k * n_parts) * stripe + (lr - k * stripe);
+}
+
+// ---- kernels -------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_frame_setup(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
+                                                    RtFrameSetup *setup, double *fr_rows)
+{
+    const int lane = threadIdx.x;
+    const int H = cam.height;
+    if (lane == 0 || lane == 1) {
+        // iter_v(H>>1, H, rot_scan_v_v, 1, false) / iter_v((H>>1)-1, -1, counter, -1, true)
+        const bool top = lane == 0;
+        const double c = cam.scan_v[0], s = top ? cam.scan_v[1] : -cam.scan_v[1];
+        double fr[3] = {cam.fr[0], cam.fr[1], cam.fr[2]}, up[3] = {cam.up[0], cam.up[1], cam.up[2]};
+        if (!top) rotate_pair(fr, up, c, s);
+        const int from = top ? (H >> 1) : (H >> 1) - 1, to = top ? H : -1, inc = top ? 1 : -1;
+        for (int y = from; y != to; y += inc) {
+            fr_rows[3 * y + 0] = fr[0];
+            fr_rows[3 * y + 1] = fr[1];
+            fr_rows[3 * y + 2] = fr[2];
+            rotate_pair(fr, up, c, s);
+        }
+    } else if (lane == 2) {
+        long long lv = 0;
+        int t = -1, oc = 0;
+        const int r = node_at_pos(S, cam.pos, t, oc, lv);
+        const int se = entity_at_pos(S, cam.pos, lv);
+        RtFrameSetup f;
+        f.fault = (r < 0 || se == -2);
+        f.start_tree = r == 1 ? t : -1;
+        f.start_oct = oc;
+        f.start_sub = se >= 0 ? S.ent_sub[se] : cfg.default_substance;
+        *setup = f;
+    }
+}
+
+// One lane per (row of this part, half).  dirs: SoA planes [3][rows*W].
+__global__ void __launch_bounds__(256) k_raygen(rt_camera_desc cam, int part, int n_parts, int stripe, int rows,
+                                                const double *__restrict__ fr_rows, double *__restrict__ dirs)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * rows) return;
+    const int lr = t >> 1;
+    const bool right = (t & 1) == 0;
+    const int W = cam.width;
+    const int y = part_row_to_y(lr, part, n_parts, stripe);
+    // iter_h(W>>1, W, y, rot_scan_h_v, fr_v, 1, false) / iter_h((W>>1)-1, -1, y, counter, fr_v, -1, true)
+    const double c = cam.scan_h[0], s = right ? cam.scan_h[1] : -cam.scan_h[1];
+    double f[3] = {fr_rows[3 * y], fr_rows[3 * y + 1], fr_rows[3 * y + 2]};
+    double l[3] = {cam.lf[0], cam.lf[1], cam.lf[2]};
+    if (!right) rotate_pair(f, l, c, s);
+    const int from = right ? (W >> 1) : (W >> 1) - 1, to = right ? W : -1, inc = right ? 1 : -1;
+    const size_t plane = (size_t)rows * (size_t)W;
+    double *row = dirs + (size_t)lr * (size_t)W;
+    for (int x = from; x != to; x += inc) {
+        row[x] = f[0];
+        row[plane + x] = f[1];
+        row[2 * plane + x] = f[2];
+        rotate_pair(f, l, c, s);
+    }
+}
+
+__device__ __forceinline__ long long wave_sum(long long v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Ray.trace for one pixel.  Output written by the caller.
+struct RayResult {
+    double rgb[3];
+    int hit_ent, hit_node, segments, status;
+};
+
+__device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg,
+                          const double cam_pos[3], const double dir0[3], RayResult &R, Counters &c)
+{
+    double o[3] = {cam_pos[0], cam_pos[1], cam_pos[2]};
+    double d[3] = {dir0[0], dir0[1], dir0[2]};
+    double col0 = 1, col1 = 1, col2 = 1;
+    int refcount = 0, cur_sub = F.start_sub;
+    bool light_hit = false;
+    double path = 0;
+    R.hit_ent = -1; R.hit_node = -1; R.segments = 1; R.status = ST_OK;
+    Walker w;
+    if (walker_set(S, w, o, d, F.start_tree >= 0, F.start_tree, F.start_oct, c) < 0) { R.status = ST_FAULT; goto done; }
+    for (;;) {
+        int node, pt, po;
+        const int r = walker_next<false>(S, w, node, pt, po, c);
+        if (r < 0) { R.status = r == -2 ? ST_CAP : ST_FAULT; goto done; }
+        if (r == 0) break;
+        // for (entity of node.value.set): first collision wins
+        const int2 ent = reinterpret_cast<const int2 *>(S.node_ent)[node];
+        int hk = -1;
+        Hit h;
+        for (int k = ent.x; k < ent.x + ent.y; k++) {
+            const RtPrim &pr = S.prim[k];
+            const int type = pr.meta & 3;
+            int got;
+            if (type == RT_ENT_FACE) { c.tri++; got = face_hit(pr.g, o, d, h); }
+            else if (type == RT_ENT_SPHERE) { c.sph++; got = sphere_hit(pr.g, o, d, h); }
+            else { c.box++; got = box_hit(pr.g, o, d, h); }
+            if (got) {
+                if (got < 0) { R.status = ST_FAULT; goto done; }
+                hk = k;
+                break;
+            }
+        }
+        if (hk < 0) continue;
+        const RtPrim &pr = S.prim[hk];
+        if (R.hit_ent < 0 && R.segments == 1) { R.hit_ent = pr.entity; R.hit_node = node; }
+        if (dot3(d[0], d[1], d[2], h.n[0], h.n[1], h.n[2]) >= 0) { R.status = ST_WARN; goto done; }  // :200-203
+        refcount++;
+        c.hit++;
+        const rt_shade sh = S.shades[pr.meta >> 2];
+        col0 = col0 * sh.rgb[0]; col1 = col1 * sh.rgb[1]; col2 = col2 * sh.rgb[2];      // mul_color
+        {
+            const double a = h.p[0] - o[0], b = h.p[1] - o[1], e = h.p[2] - o[2];
+            path += sqrt(dot3(a, b, e, a, b, e));
+        }
+        o[0] = h.p[0]; o[1] = h.p[1]; o[2] = h.p[2];
+        if (sh.light) { light_hit = true; break; }
+        if (sh.response == RT_RESP_REFLECTION) {
+            if (!sh.mirror) goto done;                          // matte: terminal
+            const double k2 = -dot3(d[0], d[1], d[2], h.n[0], h.n[1], h.n[2]) * 2;   // vector.reflection
+            d[0] = d[0] + h.n[0] * k2; d[1] = d[1] + h.n[1] * k2; d[2] = d[2] + h.n[2] * k2;
+            if (sh.roughness > 0.0) { R.status = ST_FAULT; goto done; }  // excluded by the host check
+            o[0] += d[0] * 1e-3; o[1] += d[1] * 1e-3; o[2] += d[2] * 1e-3;   // move_slightly_forward
+        } else if (sh.response == RT_RESP_TRANSMISSION) {
+            o[0] += d[0] * 1e-3; o[1] += d[1] * 1e-3; o[2] += d[2] * 1e-3;
+            const int rf = entity_at_pos(S, o, c.loc);
+            if (rf == -2) { R.status = ST_FAULT; goto done; }
+            const int sub = rf >= 0 ? S.ent_sub[rf] : cfg.default_substance;
+            if (sub >= 0) {
+                if (cur_sub < 0) { R.status = ST_FAULT; goto done; }
+                // refract_ray — src/raytracer.ts:135-150
+                const double r_ratio = S.sub_ri[cur_sub] / S.sub_ri[sub];
+                const double r_ratio_sq = r_ratio * r_ratio;
+                const double cosine = dot3(d[0], d[1], d[2], h.n[0], h.n[1], h.n[2]);
+                const double cosine_sq = cosine * cosine;
+                const double ref_sine_sq = (1 - cosine_sq) * r_ratio_sq;
+                if (ref_sine_sq <= 1) {
+                    const double ref_cosine = sqrt(1 - ref_sine_sq);
+                    const double kk = ref_cosine - cosine;
+                    const double a0 = h.n[0] * kk, a1 = h.n[1] * kk, a2 = h.n[2] * kk;
+                    d[0] *= r_ratio; d[1] *= r_ratio; d[2] *= r_ratio;
+                    d[0] -= a0; d[1] -= a1; d[2] -= a2;
+                } else {
+                    const double k2 = -dot3(d[0], d[1], d[2], h.n[0], h.n[1], h.n[2]) * 2;
+                    d[0] = d[0] + h.n[0] * k2; d[1] = d[1] + h.n[1] * k2; d[2] = d[2] + h.n[2] * k2;
+                }
+                cur_sub = sub;
+            }
+        } else {
+            goto done;
+        }
+        if (walker_set(S, w, o, d, false, 0, 0, c) < 0) { R.status = ST_FAULT; goto done; }   // :254
+        if (refcount >= cfg.refmax) { col0 = col1 = col2 = 0; goto done; }                 // COLOR_BLACK
+        R.segments++;
+    }
+    if (!light_hit) {
+        col0 = col0 * cfg.sky_rgb[0]; col1 = col1 * cfg.sky_rgb[1]; col2 = col2 * cfg.sky_rgb[2];
+    } else {
+        const double t = path * cfg.distance_attenuation_factor;
+        const double isl = 1.0 / (2.220446049250313e-16 + t * t);
+        col0 = col0 * isl; col1 = col1 * isl; col2 = col2 * isl;
+    }
+done:
+    R.rgb[0] = col0; R.rgb[1] = col1; R.rgb[2] = col2;
+}
+
+// One lane per pixel of this part; 256-lane blocks cover 16x16 pixel tiles, each wave an 8x8 tile.
+template <bool STATS>
+__global__ void __launch_bounds__(256) k_trace(RtLaunch L)
+{
+    const int W = L.cam.width;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool active = x < W && lr < L.rows;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+    RayResult R;
+    R.segments = 0; R.status = ST_OK;
+    if (active) {
+        const RtFrameSetup F = *L.setup;
+        const size_t pix = (size_t)lr * (size_t)W + (size_t)x;
+        const size_t plane = (size_t)L.rows * (size_t)W;
+        const double dir0[3] = {L.dirs[pix], L.dirs[plane + pix], L.dirs[2 * plane + pix]};
+        if (F.fault) {
+            R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.status = ST_FAULT;
+        } else {
+            trace_ray(L.scene, F, L.cfg, L.cam.pos, dir0, R, c);
+        }
+        // ExposureBuffer.set_color_i: c*w + old*(1-w), stored as f32 (src/view/exposure_buffer.ts:77-91)
+        const double wgt = L.cfg.col_weight;
+        float *px = L.rgb + 3 * pix;
+        for (int k = 0; k < 3; k++) {
+            const double old = L.blend ? (double)px[k] : 0.0;
+            double v = R.rgb[k] * wgt;
+            v += old * (1 - wgt);
+            px[k] = (float)v;
+        }
+        if (L.hit_entity) L.hit_entity[pix] = R.hit_ent;
+        if (L.hit_node) L.hit_node[pix] = R.hit_node;
+        if (L.status) L.status[pix] = (uint8_t)R.status;
+        if (R.status >= ST_FAULT && L.fault) atomicOr(L.fault, 1);
+    }
+    if (STATS) {
+        long long v[CT_N] = {active ? R.segments : 0, c.ret, c.slot, c.loc, c.sph, c.box, c.tri, c.hit,
+                             active ? 1 : 0, R.status == ST_WARN, R.status == ST_FAULT || R.status == ST_CAP};
+#pragma unroll
+        for (int k = 0; k < CT_N; k++) {
+            const long long s = wave_sum(v[k]);
+            if (lane == 0 && s) atomicAdd(L.counters + k, (unsigned long long)s);
+        }
+    }
+}
+
+template <bool INCL_UNDEF>
+__global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, double dx, double dy, double dz,
+                             int max_out, int32_t *out_tree, int32_t *out_oct, int32_t *n_out)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+    Walker w;
+    const double o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz};
+    int n = 0;
+    if (walker_set(S, w, o, d, false, 0, 0, c) < 0) { *n_out = -1; return; }
+    for (;;) {
+        int node, pt, po;
+        const int r = walker_next<INCL_UNDEF>(S, w, node, pt, po, c);
+        if (r < 0) { *n_out = -1; return; }
+        if (r == 0 || n >= max_out) break;
+        out_tree[n] = pt;
+        out_oct[n] = po == RT_OCT_UNDEF ? -1 : po;
+        n++;
+    }
+    *n_out = n;
+}
+
+}  // namespace
+
+// ---- launchers -------------------------------------------------------------------------------------------
+#define HIP_TRY(x)                                                                           \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) return rt_set_error(RT_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end)
+{
+    hipStream_t st = (hipStream_t)stream;
+    const int W = L.cam.width;
+    hipLaunchKernelGGL(k_frame_setup, dim3(1), dim3(64), 0, st, L.scene, L.cam, L.cfg, L.setup, L.fr_rows);
+    HIP_TRY(hipGetLastError());
+    if (L.rows <= 0) return RT_OK;
+    const int rg_threads = 2 * L.rows;
+    hipLaunchKernelGGL(k_raygen, dim3((rg_threads + 255) / 256), dim3(256), 0, st, L.cam, L.part, L.n_parts,
+                       L.stripe_rows, L.rows, (const double *)L.fr_rows, L.dirs);
+    HIP_TRY(hipGetLastError());
+    if (L.skip_trace) return RT_OK;
+    const dim3 grid((W + 15) / 16, (L.rows + 15) / 16);
+    if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
+    if (L.counters) hipLaunchKernelGGL(k_trace<true>, grid, dim3(256), 0, st, L);
+    else hipLaunchKernelGGL(k_trace<false>, grid, dim3(256), 0, st, L);
+    HIP_TRY(hipGetLastError());
+    if (ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
+    return RT_OK;
+}
+
+int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[3], int include_undefined,
+                         int max_out, int32_t *d_tree, int32_t *d_oct, int32_t *d_n, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    if (include_undefined)
+        hipLaunchKernelGGL(k_debug_walk<true>, dim3(1), dim3(64), 0, st, S, o[0], o[1], o[2], d[0], d[1], d[2],
+                           max_out, d_tree, d_oct, d_n);
+    else
+        hipLaunchKernelGGL(k_debug_walk<false>, dim3(1), dim3(64), 0, st, S, o[0], o[1], o[2], d[0], d[1], d[2],
+                           max_out, d_tree, d_oct, d_n);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}

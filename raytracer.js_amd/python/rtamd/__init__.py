@@ -1,0 +1,201 @@
+"""rtamd — Python binding of librt_amd.so (include/rt.h), used by bench.py, tests and smoke().
+
+The JavaScript drop-in (raytracer.js_amd/js) is the reference-facing host; this module gives the
+same C ABI to Python for measurement and parity tests.  There is no CPU fallback: if the library
+or a GPU is missing, calls raise.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "librt_amd.so")
+
+_lib = None
+
+
+class RtError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("rt error %d: %s" % (code, msg))
+        self.code = code
+
+
+def load_library(path=None):
+    """Load librt_amd.so from the package tree; raise loudly if it was not built."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError("librt_amd.so not found at %s — run __graft_entry__.build() (make -C raytracer.js_amd)" % p)
+    lib = abi.declare(C.CDLL(p))
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc):
+    if rc < 0:
+        raise RtError(rc, load_library().rt_last_error().decode(errors="replace"))
+    return rc
+
+
+def _p(a, ct):
+    return None if a is None else a.ctypes.data_as(C.POINTER(ct))
+
+
+class SceneArrays:
+    """Owns the numpy arrays an rt_scene_desc points into (keeps them alive)."""
+
+    FIELDS = ("node_pos", "node_size", "node_parent", "node_child", "node_ent_begin", "node_ent_count",
+              "list_entity", "ent_type", "ent_geom", "ent_shade", "ent_substance", "shades", "substance_ri")
+
+    def __init__(self, **arrays):
+        f64, i32 = np.float64, np.int32
+        kinds = dict(node_pos=f64, node_size=f64, node_parent=i32, node_child=i32, node_ent_begin=i32,
+                     node_ent_count=i32, list_entity=i32, ent_type=i32, ent_geom=f64, ent_shade=i32,
+                     ent_substance=i32, substance_ri=f64)
+        for k, dt in kinds.items():
+            setattr(self, k, np.ascontiguousarray(arrays[k], dtype=dt).ravel())
+        self.shades = np.ascontiguousarray(arrays["shades"], dtype=abi.SHADE_DTYPE)
+
+    @property
+    def n_nodes(self):
+        return len(self.node_size)
+
+    def desc(self):
+        d = abi.rt_scene_desc()
+        d.n_nodes = len(self.node_size)
+        d.n_list = len(self.list_entity)
+        d.n_entities = len(self.ent_type)
+        d.n_shades = len(self.shades)
+        d.n_substances = len(self.substance_ri)
+        for k in self.FIELDS:
+            a = getattr(self, k)
+            if k == "shades":
+                d.shades = a.ctypes.data_as(C.POINTER(abi.rt_shade))
+            elif a.dtype == np.float64:
+                setattr(d, k, _p(a, C.c_double))
+            else:
+                setattr(d, k, _p(a, C.c_int32))
+        self._desc = d
+        return d
+
+
+def _desc_to_arrays(d):
+    n, m, ne = d.n_nodes, d.n_list, d.n_entities
+
+    def arr(ptr, count, dt):
+        if count == 0:
+            return np.zeros(0, dt)
+        return np.ctypeslib.as_array(ptr, shape=(count,)).astype(dt, copy=True)
+    shades = np.zeros(d.n_shades, abi.SHADE_DTYPE)
+    if d.n_shades:
+        C.memmove(shades.ctypes.data, d.shades, shades.nbytes)
+    return SceneArrays(
+        node_pos=arr(d.node_pos, 3 * n, np.float64), node_size=arr(d.node_size, n, np.float64),
+        node_parent=arr(d.node_parent, n, np.int32), node_child=arr(d.node_child, 8 * n, np.int32),
+        node_ent_begin=arr(d.node_ent_begin, n, np.int32), node_ent_count=arr(d.node_ent_count, n, np.int32),
+        list_entity=arr(d.list_entity, m, np.int32), ent_type=arr(d.ent_type, ne, np.int32),
+        ent_geom=arr(d.ent_geom, 9 * ne, np.float64), ent_shade=arr(d.ent_shade, ne, np.int32),
+        ent_substance=arr(d.ent_substance, ne, np.int32), shades=shades,
+        substance_ri=arr(d.substance_ri, d.n_substances, np.float64))
+
+
+def build_scene(spec):
+    """Native add_entity_to_octree over spec.entities (in order) → SceneArrays (linearised)."""
+    L = load_library()
+    b = C.c_void_p()
+    root = (C.c_double * 3)(*spec.root_pos)
+    _check(L.rt_builder_create(root, float(spec.root_size), C.byref(b)))
+    try:
+        ents = np.ascontiguousarray(spec.entities, dtype=abi.ENTITY_DTYPE)
+        _check(L.rt_builder_add_many(b, ents.ctypes.data_as(C.POINTER(abi.rt_entity_in)), len(ents)))
+        shades = np.ascontiguousarray(spec.shades, dtype=abi.SHADE_DTYPE)
+        ri = np.ascontiguousarray(spec.substances, dtype=np.float64)
+        d = abi.rt_scene_desc()
+        _check(L.rt_builder_desc(b, shades.ctypes.data_as(C.POINTER(abi.rt_shade)), len(shades),
+                                 ri.ctypes.data_as(C.POINTER(C.c_double)), len(ri), C.byref(d)))
+        return _desc_to_arrays(d)
+    finally:
+        L.rt_builder_destroy(b)
+
+
+class Context:
+    """One rt_ctx bound to one GPU."""
+
+    def __init__(self, device=0):
+        self.L = load_library()
+        cd = abi.rt_create_desc(device=int(device), flags=0)
+        h = C.c_void_p()
+        _check(self.L.rt_create(C.byref(cd), C.byref(h)))
+        self.h = h
+        self.scene = None
+
+    def close(self):
+        if self.h:
+            self.L.rt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, scene):
+        self.scene = scene
+        _check(self.L.rt_upload_scene(self.h, C.byref(scene.desc())))
+
+    def trace_frame(self, cam, cfg, rgb=None, ids=True, stats=True, allow_fault=False):
+        P = cam.width * cam.height
+        rgb = np.zeros(P * 3, np.float32) if rgb is None else rgb
+        he = np.full(P, -7, np.int32) if ids else None
+        hn = np.full(P, -7, np.int32) if ids else None
+        st = np.full(P, 255, np.uint8) if ids else None
+        s = abi.rt_stats() if stats else None
+        rc = self.L.rt_trace_frame(self.h, C.byref(cam), C.byref(cfg), _p(rgb, C.c_float), _p(he, C.c_int32),
+                                   _p(hn, C.c_int32), _p(st, C.c_uint8), C.byref(s) if stats else None)
+        if not (allow_fault and rc == abi.RT_E_FAULT):
+            _check(rc)
+        return dict(rgb=rgb, hit_entity=he, hit_node=hn, status=st, stats=s, rc=rc)
+
+    def trace_rows_device(self, cam, cfg, part, n_parts, stripe, d_rgb_ptr, stream_ptr=None, stats=False):
+        rows = C.c_int32()
+        s = abi.rt_stats() if stats else None
+        _check(self.L.rt_trace_rows_device(self.h, C.byref(cam), C.byref(cfg), int(part), int(n_parts), int(stripe),
+                                           C.c_void_p(d_rgb_ptr), C.c_void_p(stream_ptr) if stream_ptr else None,
+                                           C.byref(rows), C.byref(s) if stats else None))
+        return rows.value, s
+
+    def kernel_times(self, n):
+        out = np.zeros(n)
+        k = _check(self.L.rt_kernel_times(self.h, _p(out, C.c_double), int(n)))
+        return out[:k]
+
+    def debug_walk(self, origin, d, include_undefined=True, max_out=4096):
+        o = (C.c_double * 3)(*origin)
+        dd = (C.c_double * 3)(*d)
+        tr = np.zeros(max_out, np.int32)
+        oc = np.zeros(max_out, np.int32)
+        n = C.c_int32()
+        _check(self.L.rt_debug_walk(self.h, o, dd, int(include_undefined), int(max_out), _p(tr, C.c_int32),
+                                    _p(oc, C.c_int32), C.byref(n)))
+        return list(zip(tr[:n.value].tolist(), oc[:n.value].tolist()))
+
+    def camera_dirs(self, cam):
+        out = np.zeros(cam.width * cam.height * 3)
+        _check(self.L.rt_debug_camera_dirs(self.h, C.byref(cam), _p(out, C.c_double)))
+        return out
+
+
+def part_rows(H, part, n_parts, stripe):
+    """Global row indices owned by `part` in stripe order (mirrors rt_part_rows)."""
+    rows = []
+    n_stripes = (H + stripe - 1) // stripe
+    for s in range(part, n_stripes, n_parts):
+        rows.extend(range(s * stripe, min(H, (s + 1) * stripe)))
+    return np.array(rows, dtype=np.int64)

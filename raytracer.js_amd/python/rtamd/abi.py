@@ -1,0 +1,120 @@
+"""ctypes mirror of include/rt.h (plain-data descriptors + prototypes of librt_amd.so).
+
+The layouts here must match include/rt.h byte for byte; tests/test_abi.py checks the sizes the
+library reports against them.
+"""
+import ctypes as C
+
+import numpy as np
+
+RT_OK = 0
+RT_E_INVALID = -1
+RT_E_HIP = -2
+RT_E_UNSUPPORTED = -3
+RT_E_NOSCENE = -4
+RT_E_FAULT = -5
+RT_E_NODEVICE = -6
+RT_E_TREE = -7
+
+RT_ENT_SPHERE, RT_ENT_BOX, RT_ENT_FACE = 0, 1, 2
+RT_RESP_REFLECTION, RT_RESP_TRANSMISSION, RT_RESP_BOTH = 0, 1, 2
+
+STATUS_OK, STATUS_WARN, STATUS_FAULT, STATUS_CAP = 0, 1, 2, 3
+
+_d = C.c_double
+_i = C.c_int32
+_pd = C.POINTER(C.c_double)
+_pi = C.POINTER(C.c_int32)
+
+
+class rt_shade(C.Structure):
+    _fields_ = [("response", _i), ("light", _i), ("mirror", _i), ("pad_", _i),
+                ("roughness", _d), ("rgb", _d * 3)]
+
+
+SHADE_DTYPE = np.dtype([("response", "<i4"), ("light", "<i4"), ("mirror", "<i4"), ("pad_", "<i4"),
+                        ("roughness", "<f8"), ("rgb", "<f8", (3,))])
+assert SHADE_DTYPE.itemsize == C.sizeof(rt_shade)
+
+
+class rt_scene_desc(C.Structure):
+    _fields_ = [("n_nodes", _i), ("n_list", _i), ("n_entities", _i), ("n_shades", _i),
+                ("n_substances", _i), ("pad_", _i),
+                ("node_pos", _pd), ("node_size", _pd), ("node_parent", _pi), ("node_child", _pi),
+                ("node_ent_begin", _pi), ("node_ent_count", _pi), ("list_entity", _pi),
+                ("ent_type", _pi), ("ent_geom", _pd), ("ent_shade", _pi), ("ent_substance", _pi),
+                ("shades", C.POINTER(rt_shade)), ("substance_ri", _pd)]
+
+
+class rt_camera_desc(C.Structure):
+    _fields_ = [("width", _i), ("height", _i), ("pos", _d * 3), ("fr", _d * 3), ("lf", _d * 3),
+                ("up", _d * 3), ("scan_h", _d * 2), ("scan_v", _d * 2)]
+
+
+class rt_config_desc(C.Structure):
+    _fields_ = [("refmax", _i), ("default_substance", _i), ("sky_rgb", _d * 3),
+                ("distance_attenuation_factor", _d), ("col_weight", _d)]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [("segments", C.c_int64), ("n_ret", C.c_int64), ("n_slot", C.c_int64),
+                ("n_loc", C.c_int64), ("n_sph", C.c_int64), ("n_box", C.c_int64),
+                ("n_tri", C.c_int64), ("n_hit", C.c_int64), ("primary", C.c_int64),
+                ("n_warn", C.c_int64), ("n_fault", C.c_int64), ("kernel_ms", _d), ("frame_ms", _d)]
+
+    COUNTERS = ("segments", "n_ret", "n_slot", "n_loc", "n_sph", "n_box", "n_tri", "n_hit",
+                "primary", "n_warn", "n_fault")
+
+    def counters(self):
+        return {k: int(getattr(self, k)) for k in self.COUNTERS}
+
+
+class rt_create_desc(C.Structure):
+    _fields_ = [("device", _i), ("flags", _i)]
+
+
+class rt_entity_in(C.Structure):
+    _fields_ = [("type", _i), ("shade", _i), ("substance", _i), ("max_in_depth", _i),
+                ("max_out_depth", _i), ("pad_", _i), ("geom", _d * 9)]
+
+
+ENTITY_DTYPE = np.dtype([("type", "<i4"), ("shade", "<i4"), ("substance", "<i4"),
+                         ("max_in_depth", "<i4"), ("max_out_depth", "<i4"), ("pad_", "<i4"),
+                         ("geom", "<f8", (9,))])
+assert ENTITY_DTYPE.itemsize == C.sizeof(rt_entity_in)
+
+# Every symbol include/rt.h declares (checked by tests/test_abi.py).
+EXPORTS = ("rt_create", "rt_destroy", "rt_last_error", "rt_abi_version", "rt_upload_scene",
+           "rt_trace_frame", "rt_trace_rows_device", "rt_kernel_times", "rt_debug_walk",
+           "rt_debug_camera_dirs", "rt_builder_create", "rt_builder_destroy", "rt_builder_add",
+           "rt_builder_add_many", "rt_builder_desc")
+
+
+def declare(lib):
+    """Attach argtypes/restype for every export of librt_amd.so."""
+    P = C.POINTER
+    vp = C.c_void_p
+    lib.rt_create.argtypes = [P(rt_create_desc), P(vp)]
+    lib.rt_destroy.argtypes = [vp]
+    lib.rt_destroy.restype = None
+    lib.rt_last_error.restype = C.c_char_p
+    lib.rt_abi_version.restype = C.c_int
+    lib.rt_upload_scene.argtypes = [vp, P(rt_scene_desc)]
+    lib.rt_trace_frame.argtypes = [vp, P(rt_camera_desc), P(rt_config_desc), P(C.c_float), _pi, _pi,
+                                   P(C.c_uint8), P(rt_stats)]
+    lib.rt_trace_rows_device.argtypes = [vp, P(rt_camera_desc), P(rt_config_desc), _i, _i, _i, vp, vp,
+                                         _pi, P(rt_stats)]
+    lib.rt_kernel_times.argtypes = [vp, _pd, _i]
+    lib.rt_debug_walk.argtypes = [vp, _pd, _pd, _i, _i, _pi, _pi, _pi]
+    lib.rt_debug_camera_dirs.argtypes = [vp, P(rt_camera_desc), _pd]
+    lib.rt_builder_create.argtypes = [_pd, _d, P(vp)]
+    lib.rt_builder_destroy.argtypes = [vp]
+    lib.rt_builder_destroy.restype = None
+    lib.rt_builder_add.argtypes = [vp, P(rt_entity_in), _pi]
+    lib.rt_builder_add_many.argtypes = [vp, P(rt_entity_in), _i]
+    lib.rt_builder_desc.argtypes = [vp, P(rt_shade), _i, _pd, _i, P(rt_scene_desc)]
+    return lib
+
+
+def as_ptr(arr, ctype):
+    return arr.ctypes.data_as(C.POINTER(ctype))

@@ -1,0 +1,218 @@
+"""HIP path vs the oracle, through the C ABI, on a real MI355X.
+
+Bar (BASELINE.json north_star): RGB within 1e-4 per channel, bit-exact hit entity id and octree
+node id.  The kernels mirror the reference's binary64 operation order, so the RGB comparison is
+also checked for exact equality of the f32 ExposureBuffer values.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+import rtamd
+from rtamd import abi, scenes
+
+pytestmark = pytest.mark.gpu
+
+RGB_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = rtamd.Context(0)
+    yield c
+    c.close()
+
+
+def _compare(ref, got, pixels=None, exact_rgb=True):
+    P = len(got["hit_entity"])
+    idx = np.arange(P) if pixels is None else np.asarray(pixels)
+    rr = ref["rgb"].reshape(-1, 3)[idx]
+    gg = got["rgb"].reshape(-1, 3)[idx]
+    diff = np.abs(rr.astype(np.float64) - gg.astype(np.float64))
+    assert np.all(np.isfinite(gg)), "non-finite output"
+    assert diff.max() <= RGB_TOL, "max |drgb| %g at %s" % (diff.max(), idx[np.argmax(diff.max(1))])
+    assert np.array_equal(ref["hit_entity"][idx], got["hit_entity"][idx])
+    assert np.array_equal(ref["hit_node"][idx], got["hit_node"][idx])
+    assert np.array_equal(ref["status"][idx], got["status"][idx])
+    if exact_rgb:
+        assert np.array_equal(rr.view(np.uint32), gg.view(np.uint32)), "%d pixels not bit-identical" % int(
+            (rr.view(np.uint32) != gg.view(np.uint32)).any(1).sum())
+
+
+def _run_both(ctx, spec, cam, cfg, pixels=None, nthreads=8):
+    w, root = oracle.build_scene(spec)
+    ref = w.trace_frame(root, cam, cfg, pixels=pixels, nthreads=nthreads)
+    ctx.upload(rtamd.build_scene(spec))
+    got = ctx.trace_frame(cam, cfg, allow_fault=True)
+    return ref, got
+
+
+# ---- walker KATs on the device (rt_debug_walk) --------------------------------------------------------
+def _kat_scene(subtrees):
+    """Root [0,1)^3 with direct subtrees at the given octants, no entities (DFS ids 1.. in octant order)."""
+    n = 1 + len(subtrees)
+    pos = np.zeros((n, 3))
+    size = np.ones(n)
+    parent = np.full(n, -1, np.int32)
+    child = np.full((n, 8), -1, np.int32)
+    for k, o in enumerate(sorted(subtrees)):
+        i = k + 1
+        pos[i] = [0.5 * ((o >> a) & 1) for a in range(3)]
+        size[i] = 0.5
+        parent[i] = 0
+        child[0, o] = i
+    return rtamd.SceneArrays(node_pos=pos, node_size=size, node_parent=parent, node_child=child,
+                             node_ent_begin=np.zeros(n), node_ent_count=np.zeros(n), list_entity=np.zeros(0),
+                             ent_type=np.zeros(0), ent_geom=np.zeros(0), ent_shade=np.zeros(0),
+                             ent_substance=np.zeros(0), shades=scenes._shade(), substance_ri=scenes.SUBSTANCES)
+
+
+def test_walker_two_level_kat_gpu(ctx, kats):
+    """test/octree-space-walker.test.ts:57-70 on the GPU walker."""
+    k = kats["walker_two_level"]
+    ctx.upload(_kat_scene(list(k["subtrees"].values())))
+    ids = {"tree": 0, "s1": 1, "s2": 2, "s3": 3}
+    stops = ctx.debug_walk(k["pos"], k["dir"], include_undefined=True)
+    assert stops[-1] == (0, -1)
+    assert stops[:-1] == [(ids[t], o) for t, o in k["expect"]]
+
+
+def test_walker_one_level_kat_gpu(ctx, kats):
+    ctx.upload(_kat_scene([]))
+    dirs = {29: (3 / 4, math.sqrt(3) / 4, 0), 31: (5, 3, 2), 32: (1, 1, 1), 35: (2, 1.0, 4)}
+    for case in kats["walker_one_level"]["cases"]:
+        stops = ctx.debug_walk(case["pos"], dirs[case["line"]], include_undefined=True)
+        assert [o for _, o in stops[:-1]] == case["expect_octants"]
+    eps = 2.0 ** -52
+    for pos, d in (((1, 1, 0), (-3 / 4, -math.sqrt(3) / 4, 0)), ((1 + eps, 1, 1 - eps), (-1, -1, -1)),
+                   ((1, 1, 1), (-1, -1, -1))):
+        assert ctx.debug_walk(pos, d, include_undefined=True) == [(0, -1)]
+
+
+def test_walker_matches_oracle_random_rays(ctx):
+    """Random rays through a built scene tree: identical stop sequences (include_undefined both ways)."""
+    spec = scenes.small_random(7)
+    ctx.upload(rtamd.build_scene(spec))
+    w, root = oracle.build_scene(spec)
+    w.linearize(root)
+    rng = np.random.default_rng(3)
+    for inc in (True, False):
+        wk = w.walker(root, include_undefined=inc)
+        for _ in range(200):
+            o = rng.uniform(-0.2, 1.2, 3)
+            d = rng.normal(size=3)
+            got = ctx.debug_walk(o.tolist(), d.tolist(), include_undefined=inc)
+            ref = [(w.tree_id(pt), -1 if po is None else po) for _, pt, po in w.walk(wk, o.tolist(), d.tolist())]
+            assert got == ref
+
+
+# ---- ray generation --------------------------------------------------------------------------------------
+@pytest.mark.parametrize("wh", [(256, 256), (1920, 1080), (101, 37), (2, 1)])
+def test_camera_dirs_bit_exact(ctx, wh):
+    ctx.upload(rtamd.build_scene(scenes.config1_spheres()))
+    cam = scenes.make_camera(*wh)
+    ref = oracle.camera_dirs(cam)
+    got = ctx.camera_dirs(cam)
+    assert np.array_equal(ref.view(np.uint64), got.view(np.uint64))
+
+
+# ---- full frames -------------------------------------------------------------------------------------------
+def test_config1_full_frame(ctx):
+    spec = scenes.config1_spheres()
+    cam, cfg = scenes.make_camera(256, 256), scenes.make_config(2)
+    ref, got = _run_both(ctx, spec, cam, cfg)
+    _compare(ref, got)
+    assert got["stats"].counters() == ref["counters"]
+
+
+@pytest.mark.parametrize("refmax", [1, 2, 4])
+def test_config1_refmax(ctx, refmax):
+    spec = scenes.config1_spheres()
+    cam, cfg = scenes.make_camera(128, 96), scenes.make_config(refmax)
+    ref, got = _run_both(ctx, spec, cam, cfg)
+    _compare(ref, got)
+    assert got["stats"].counters() == ref["counters"]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
+def test_small_random_scenes(ctx, seed):
+    spec = scenes.small_random(seed)
+    cam, cfg = scenes.make_camera(160, 120), scenes.make_config(3)
+    ref, got = _run_both(ctx, spec, cam, cfg)
+    _compare(ref, got)
+    assert got["stats"].counters() == ref["counters"]
+
+
+def test_camera_outside_root(ctx):
+    """Camera outside the root: the walker yields only the root (src/octree_space.ts:254-286)."""
+    spec = scenes.small_random(11)
+    cam = scenes.make_camera(96, 64, pos=(-0.4, 0.3, 0.45))
+    cfg = scenes.make_config(2)
+    ref, got = _run_both(ctx, spec, cam, cfg)
+    _compare(ref, got)
+
+
+def test_exposure_blend(ctx):
+    """ExposureBuffer.next_frame weight 1/(1+n): c*w + old*(1-w) in f64, stored as f32."""
+    spec = scenes.small_random(2)
+    cam = scenes.make_camera(64, 48)
+    cfg = scenes.make_config(2, col_weight=1 / 3)
+    rng = np.random.default_rng(0)
+    old = rng.uniform(0, 2, 64 * 48 * 3).astype(np.float32)
+    w, root = oracle.build_scene(spec)
+    ref = w.trace_frame(root, cam, cfg, rgb=old.copy())
+    ctx.upload(rtamd.build_scene(spec))
+    got = ctx.trace_frame(cam, cfg, rgb=old.copy())
+    _compare(ref, got)
+
+
+def test_transmission_scene(ctx):
+    """TRANSMISSION materials: entity_at_pos + refract_ray (src/raytracer.ts:135-150,238-249)."""
+    spec = scenes.small_random(5)
+    sh = spec.shades.copy()
+    sh["response"][::3] = abi.RT_RESP_TRANSMISSION
+    sh["light"][::3] = 0
+    ents = spec.entities.copy()
+    ents["substance"][::2] = 2          # GLASS
+    ents["substance"][1::7] = -1        # undefined substance
+    spec = scenes.SceneSpec("transmission", ents, sh)
+    cam, cfg = scenes.make_camera(128, 128), scenes.make_config(5)
+    ref, got = _run_both(ctx, spec, cam, cfg)
+    _compare(ref, got)
+    assert got["stats"].counters() == ref["counters"]
+
+
+def test_roughness_rejected(ctx):
+    spec = scenes.config1_spheres()
+    sh = spec.shades.copy()
+    sh["roughness"][1] = 0.5            # a mirror
+    ctx.upload(rtamd.build_scene(scenes.SceneSpec("rough", spec.entities, sh)))
+    with pytest.raises(rtamd.RtError) as ei:
+        ctx.trace_frame(scenes.make_camera(16, 16), scenes.make_config(2))
+    assert ei.value.code == abi.RT_E_UNSUPPORTED
+
+
+# ---- BASELINE configs at full size (sampled oracle pixels) ---------------------------------------------------
+def _sample(W, H, n, seed):
+    rng = np.random.default_rng(seed)
+    pix = rng.choice(W * H, n, replace=False)
+    rows = np.arange(W) + (H // 2) * W                       # plus one full row
+    return np.unique(np.concatenate([pix, rows]))
+
+
+@pytest.mark.parametrize("name", ["config2", "config3"])
+def test_baseline_config_sampled(ctx, name):
+    factory, W, H, refmax = scenes.WORKLOADS[name]
+    spec = factory()
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
+    pix = _sample(W, H, 6000, 1)
+    ref, got = _run_both(ctx, spec, cam, cfg, pixels=pix)
+    _compare(ref, got, pixels=pix)
+    assert got["rc"] == 0
+    st = got["stats"]
+    assert st.primary == W * H and st.n_fault == 0
+    # size-independent properties on the full frame
+    assert np.all(got["status"] <= 1)
+    assert np.all((got["hit_entity"] >= -1) & (got["hit_entity"] < len(spec.entities)))
