@@ -1,0 +1,87 @@
+"""The JavaScript drop-in (raytracer.js_amd/js/raytracer.js): a `Raytracer` with the reference's
+constructor and trace_frame() (src/raytracer.ts:281-339) that reads reference-shaped scene objects,
+flattens them, and renders through the N-API addon into ExposureBuffer.pixels.
+
+CPU: the flattening reproduces the native builder's arrays bit for bit.
+GPU: one frame through node -> N-API -> librt_amd.so equals the oracle.
+"""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import rtamd
+from rtamd import scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RUNNER = os.path.join(ROOT, "tests", "js", "run_dropin.js")
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
+
+
+def _dump(tmp_path, spec, cam, cfg):
+    s = rtamd.build_scene(spec)
+    sc = {k: getattr(s, k).tolist() for k in ("node_pos", "node_size", "node_parent", "node_child", "node_ent_begin",
+                                             "node_ent_count", "list_entity", "ent_type", "ent_geom", "ent_shade",
+                                             "ent_substance", "substance_ri")}
+    sc["shades"] = [dict(response=int(x["response"]), light=int(x["light"]), mirror=int(x["mirror"]),
+                         roughness=float(x["roughness"]), rgb=[float(v) for v in x["rgb"]]) for x in s.shades]
+    sc["cam"] = dict(width=cam.width, height=cam.height, pos=list(cam.pos), fr=list(cam.fr), lf=list(cam.lf),
+                     up=list(cam.up), scan_h=list(cam.scan_h), scan_v=list(cam.scan_v))
+    sc["cfg"] = dict(refmax=cfg.refmax, default_substance=cfg.default_substance, atten=cfg.distance_attenuation_factor,
+                     sky=list(cfg.sky_rgb))
+    p = tmp_path / "scene.json"
+    p.write_text(json.dumps(sc))
+    return str(p)
+
+
+def _node(args, timeout=600):
+    r = subprocess.run([NODE] + args, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+@pytest.mark.parametrize("name", ["config1", "small3", "config2"])
+def test_serialize_matches_native_builder(tmp_path, name):
+    spec = {"config1": scenes.config1_spheres, "small3": lambda: scenes.small_random(3),
+            "config2": scenes.config2}[name]()
+    path = _dump(tmp_path, spec, scenes.make_camera(8, 8), scenes.make_config(2))
+    out = _node([RUNNER, path, str(tmp_path / "out"), "--serialize-only"])
+    assert "serialize ok" in out
+
+
+def test_addon_loads_and_fails_loudly_without_gpu():
+    """The addon loads; with no GPU create() throws RT_E_NODEVICE (never a silent CPU path)."""
+    js = ("const rt=require(%r);const a=rt.load_addon();"
+          "if(a.abiVersion()!==1)throw Error('abi');"
+          "try{a.create(0);console.log('GPU')}catch(e){console.log(e.code)}") % os.path.join(ROOT, "raytracer.js_amd", "js", "raytracer.js")
+    out = _node(["-e", js]).strip()
+    assert out in ("GPU", "RT_E_NODEVICE")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,wh,refmax", [("config1", (256, 256), 2), ("small4", (200, 150), 3)])
+def test_dropin_frame_equals_oracle(tmp_path, name, wh, refmax):
+    spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4)}[name]()
+    cam, cfg = scenes.make_camera(*wh), scenes.make_config(refmax)
+    path = _dump(tmp_path, spec, cam, cfg)
+    _node([RUNNER, path, str(tmp_path / "out")])
+    P = wh[0] * wh[1]
+    rgb = np.fromfile(tmp_path / "out.rgb", dtype=np.float32)
+    ent = np.fromfile(tmp_path / "out.ent", dtype=np.int32)
+    node = np.fromfile(tmp_path / "out.node", dtype=np.int32)
+    status = np.fromfile(tmp_path / "out.status", dtype=np.uint8)
+    assert rgb.size == 3 * P and ent.size == P
+    w, root = oracle.build_scene(spec)
+    ref = w.trace_frame(root, cam, cfg, nthreads=8)
+    assert np.abs(rgb.astype(np.float64) - ref["rgb"]).max() <= 1e-4
+    assert np.array_equal(rgb.view(np.uint32), ref["rgb"].view(np.uint32))
+    assert np.array_equal(ent, ref["hit_entity"])
+    assert np.array_equal(node, ref["hit_node"])
+    assert np.array_equal(status, ref["status"])
+    stats = json.loads((tmp_path / "out.json").read_text())["stats"]
+    assert stats["segments"] == ref["counters"]["segments"]
