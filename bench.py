@@ -29,12 +29,17 @@ import rtamd  # noqa: E402  (after torch: share its HIP runtime)
 from rtamd import scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-# Algorithmic bytes per unit of work (canonical f64 layout).
-BYTES = dict(n_ret=48, n_slot=32, n_loc=40, n_sph=36, n_box=36, n_tri=76, n_hit=40, primary=12)
+# Algorithmic bytes per unit of work of the reference's algorithm (canonical f64
+# layout) over the reference-equivalent counters: what the in-order entity scan would read.
+BYTES_REF = dict(n_ret=48, n_slot=32, n_loc=40, n_sph=36, n_box=36, n_tri=76, n_hit=40, primary=12)
+# Algorithmic bytes of the work k_trace actually performs: walker records as above,
+# 32 B per cull-hierarchy box test, 80 B per exact entity test (record + rank), 44 B per hit (shade
+# record + entity id), 36 B per pixel (24 B direction read + 12 B RGB store).
+BYTES_KERNEL = dict(n_ret=48, n_slot=32, n_loc=40, n_cull=32, n_exact=80, n_hit=44, primary=36)
 
 
-def algorithmic_bytes(counters):
-    return sum(BYTES[k] * counters[k] for k in BYTES)
+def algorithmic_bytes(counters, table):
+    return sum(table[k] * counters[k] for k in table)
 
 
 def cpu_baseline(spec, cam, cfg, budget_s):
@@ -118,12 +123,14 @@ def main():
 
     # work counters of one frame (untimed STATS launch): segments and algorithmic bytes
     _, st = ctx.trace_rows_device(cam, cfg, rank, world, args.stripe, local_buf.data_ptr(), sp, stats=True)
-    counters = st.counters()
-    ctr = torch.tensor([counters[k] for k in st.COUNTERS], dtype=torch.int64, device=dev)
+    counters = dict(st.counters(), **st.work())
+    names = st.COUNTERS + st.WORK
+    ctr = torch.tensor([counters[k] for k in names], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(ctr)
-    tot = dict(zip(st.COUNTERS, ctr.tolist()))
-    local_bytes = algorithmic_bytes(counters)
+    tot = dict(zip(names, ctr.tolist()))
+    local_bytes = algorithmic_bytes(counters, BYTES_KERNEL)
+    local_bytes_ref = algorithmic_bytes(counters, BYTES_REF)
 
     for _ in range(args.warmup):
         step()
@@ -152,7 +159,9 @@ def main():
     roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=(achieved / HBM_PEAK_GBS) if achieved else None, traffic=None,
                     kernel="k_trace", kernel_ms=k_ms, bytes_per_launch=local_bytes,
-                    bytes_formula="48*n_ret+32*n_slot+40*n_loc+36*n_sph+36*n_box+76*n_tri+40*n_hit+12*primary")
+                    bytes_formula="48*n_ret+32*n_slot+40*n_loc+32*n_cull+80*n_exact+44*n_hit+36*primary",
+                    bytes_reference_equivalent=local_bytes_ref,
+                    reference_equivalent_formula="SURVEY 8d: 48*n_ret+32*n_slot+40*n_loc+36*n_sph+36*n_box+76*n_tri+40*n_hit+12*primary")
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:

@@ -136,6 +136,11 @@ typedef struct rt_stats {
     int64_t primary;    /* primary rays (= pixels traced)                                    */
     int64_t n_warn;     /* rays ended by the acute-normal warning (src/raytracer.ts:200-203) */
     int64_t n_fault;    /* rays that reached a reference throw                              */
+    /* Work the GPU actually performed.  n_sph/n_box/n_tri above are the tests the reference
+     * performs (Set order up to the first hit), reproduced exactly; the GPU culls with per-node
+     * bounding hierarchies and runs the exact binary64 test only on candidates. */
+    int64_t n_cull;     /* conservative f32 box tests of the per-node cull hierarchies      */
+    int64_t n_exact;    /* exact binary64 entity tests executed                             */
     double  kernel_ms;  /* trace kernel time of this call (HIP events)                      */
     double  frame_ms;   /* whole call, host wall                                            */
 } rt_stats;
@@ -145,8 +150,12 @@ typedef struct rt_ctx rt_ctx;
 
 typedef struct rt_create_desc {
     int32_t device;       /* HIP device ordinal */
-    int32_t flags;        /* reserved, 0        */
+    int32_t flags;        /* RT_CREATE_*        */
 } rt_create_desc;
+
+/* Disable the per-node cull hierarchies: every entity of a returned node runs the exact test
+ * (verification mode; results are identical by construction). */
+#define RT_CREATE_NO_CULL 1
 
 int  rt_create(const rt_create_desc *desc, rt_ctx **out);
 void rt_destroy(rt_ctx *ctx);

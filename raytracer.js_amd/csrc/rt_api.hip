@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -64,13 +65,19 @@ struct DevBuf {
 
 }  // namespace
 
+int rt_build_cull(const rt_scene_desc *s, std::vector<RtPrim> &prim, std::vector<RtBvh> &bvh,
+                  std::vector<int32_t> &node_ent, std::vector<int32_t> &prefix, int leaf);
+
 struct rt_ctx {
     int device = 0;
+    int flags = 0;
+    int bvh_leaf = 4;
     hipStream_t stream = nullptr;
     bool has_scene = false;
     bool scatter = false;            // a mirror shade with roughness > 0 is reachable
     RtDevScene scene{};
     DevBuf b_node_ps, b_node_child, b_node_up, b_node_ent, b_prim, b_shades, b_ent_sub, b_sub_ri;
+    DevBuf b_bvh, b_list, b_prefix;
     DevBuf b_setup, b_fr, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
     DevBuf b_walk;
     static constexpr int NEV = 256;
@@ -95,6 +102,10 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     rt_ctx *c = new (std::nothrow) rt_ctx();
     if (!c) return rt_set_error(RT_E_INVALID, "rt_create: out of memory");
     c->device = dev;
+    c->flags = desc ? desc->flags : 0;
+    if (const char *e = getenv("RT_NO_CULL"))
+        if (e[0] == '1') c->flags |= RT_CREATE_NO_CULL;
+    if (const char *e = getenv("RT_BVH_LEAF")) c->bvh_leaf = atoi(e);
     int r = use_device(c);
     if (r == RT_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         r = rt_set_error(RT_E_HIP, "rt_create: hipStreamCreate failed");
@@ -120,7 +131,7 @@ extern "C" void rt_destroy(rt_ctx *c)
     DevBuf *bufs[] = {&c->b_node_ps, &c->b_node_child, &c->b_node_up, &c->b_node_ent, &c->b_prim,
                       &c->b_shades, &c->b_ent_sub, &c->b_sub_ri, &c->b_setup, &c->b_fr, &c->b_dirs,
                       &c->b_rgb, &c->b_hit_e, &c->b_hit_n, &c->b_status, &c->b_counters, &c->b_fault,
-                      &c->b_walk};
+                      &c->b_walk, &c->b_bvh, &c->b_list, &c->b_prefix};
     for (DevBuf *b : bufs) b->release();
     for (int i = 0; i < rt_ctx::NEV; i++)
         for (int k = 0; k < 2; k++)
@@ -214,18 +225,27 @@ extern "C" int rt_upload_scene(rt_ctx *c, const rt_scene_desc *s)
             }
         }
         p.meta = type | (s->ent_shade[e] << 2);
-        p.entity = e;
+        p.rank = k;
         const rt_shade &sh = s->shades[s->ent_shade[e]];
         if (!sh.light && sh.response == RT_RESP_REFLECTION && sh.mirror && sh.roughness > 0.0) scatter = true;
     }
-    int r = use_device(c);
+    (void)ent;
+    // per-node cull hierarchies; prims are re-ordered within each node's range
+    std::vector<RtBvh> bvh;
+    std::vector<int32_t> ent4, prefix;
+    if (NL == 0) prim.clear();
+    int r = rt_build_cull(s, prim, bvh, ent4, prefix, c->bvh_leaf);
     if (r != RT_OK) return r;
+    if ((r = use_device(c)) != RT_OK) return r;
     c->has_scene = false;
     if ((r = upload(c, c->b_node_ps, ps.data(), ps.size())) != RT_OK) return r;
     if ((r = upload(c, c->b_node_child, s->node_child, 8 * (size_t)N)) != RT_OK) return r;
     if ((r = upload(c, c->b_node_up, up.data(), up.size())) != RT_OK) return r;
-    if ((r = upload(c, c->b_node_ent, ent.data(), ent.size())) != RT_OK) return r;
+    if ((r = upload(c, c->b_node_ent, ent4.data(), ent4.size())) != RT_OK) return r;
     if ((r = upload(c, c->b_prim, prim.data(), prim.size())) != RT_OK) return r;
+    if ((r = upload(c, c->b_bvh, bvh.data(), bvh.size())) != RT_OK) return r;
+    if ((r = upload(c, c->b_list, s->list_entity, (size_t)NL)) != RT_OK) return r;
+    if ((r = upload(c, c->b_prefix, prefix.data(), prefix.size())) != RT_OK) return r;
     if ((r = upload(c, c->b_shades, s->shades, (size_t)s->n_shades)) != RT_OK) return r;
     if ((r = upload(c, c->b_ent_sub, s->ent_substance, (size_t)NE)) != RT_OK) return r;
     if ((r = upload(c, c->b_sub_ri, s->substance_ri, (size_t)s->n_substances)) != RT_OK) return r;
@@ -236,10 +256,14 @@ extern "C" int rt_upload_scene(rt_ctx *c, const rt_scene_desc *s)
     d.node_up = (const int32_t *)c->b_node_up.p;
     d.node_ent = (const int32_t *)c->b_node_ent.p;
     d.prim = (const RtPrim *)c->b_prim.p;
+    d.bvh = (const RtBvh *)c->b_bvh.p;
+    d.list_entity = (const int32_t *)c->b_list.p;
+    d.list_prefix = (const int32_t *)c->b_prefix.p;
     d.shades = (const rt_shade *)c->b_shades.p;
     d.ent_sub = (const int32_t *)c->b_ent_sub.p;
     d.sub_ri = (const double *)c->b_sub_ri.p;
     d.n_nodes = N; d.n_list = NL; d.n_entities = NE; d.n_shades = s->n_shades; d.n_subs = s->n_substances;
+    d.n_bvh = (int32_t)bvh.size();
     c->scatter = scatter;
     c->has_scene = true;
     return RT_OK;
@@ -289,6 +313,7 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.hit_node = want_ids ? (int32_t *)c->b_hit_n.p : nullptr;
     L.status = want_ids ? (uint8_t *)c->b_status.p : nullptr;
     L.fault = (int32_t *)c->b_fault.p;
+    L.cull = (c->flags & RT_CREATE_NO_CULL) ? 0 : 1;
     return RT_OK;
 }
 
@@ -298,6 +323,7 @@ static void fill_stats(rt_stats *st, const unsigned long long *h)
     st->n_loc = (int64_t)h[CT_LOC]; st->n_sph = (int64_t)h[CT_SPH]; st->n_box = (int64_t)h[CT_BOX];
     st->n_tri = (int64_t)h[CT_TRI]; st->n_hit = (int64_t)h[CT_HIT]; st->primary = (int64_t)h[CT_PRIM];
     st->n_warn = (int64_t)h[CT_WARN]; st->n_fault = (int64_t)h[CT_FAULT];
+    st->n_cull = (int64_t)h[CT_CULL]; st->n_exact = (int64_t)h[CT_EXACT];
 }
 
 extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,

@@ -1,0 +1,183 @@
+// rt_cull.cpp — per-node cull hierarchies for rt_upload_scene.
+//
+// The reference tests a returned node's entities in EntitySet order and keeps the first one that
+// reports a collision (src/raytracer.ts:186-195).  The GPU reaches the same entity with less work:
+// each node's entity list gets a small binary BVH whose boxes are the entities' AABBs widened by
+// a margin `delta` and rounded outward to f32.  Only entities whose box the ray's half-line
+// crosses run the exact binary64 test, and the hit with the smallest Set rank wins — the entity
+// the reference's in-order loop stops at.  Entities whose exact test can be ill-conditioned
+// (degenerate triangles, non-finite geometry) get an infinite box and are always tested.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "rt.h"
+#include "rt_internal.h"
+
+namespace {
+
+struct Item {
+    double lo[3], hi[3], c[3];
+    int slot;           // index into the node's original (Set-order) prim records
+};
+
+float round_down(double x)
+{
+    float f = (float)x;
+    if (isnan(x)) return -INFINITY;
+    if ((double)f > x) f = nextafterf(f, -INFINITY);
+    return f;
+}
+
+float round_up(double x)
+{
+    float f = (float)x;
+    if (isnan(x)) return INFINITY;
+    if ((double)f < x) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+// Conservative AABB of one primitive record (RtPrim layout), widened by delta.
+void prim_bounds(const RtPrim &p, double delta, Item &it)
+{
+    const int type = p.meta & 3;
+    const double *g = p.g;
+    bool finite = true;
+    if (type == RT_ENT_SPHERE) {
+        // |2/d| recovers |d|: r = |d|/2 = 1/|k|
+        const double r = 1.0 / fabs(g[6]);
+        for (int i = 0; i < 3; i++) { it.lo[i] = g[i] - r; it.hi[i] = g[i] + r; }
+        finite = isfinite(r);
+    } else if (type == RT_ENT_BOX) {
+        const double h = fabs(g[3]) * 0.5;
+        for (int i = 0; i < 3; i++) { it.lo[i] = g[i] - h; it.hi[i] = g[i] + h; }
+    } else {
+        double l1 = 0, l2 = 0, l3 = 0;
+        for (int i = 0; i < 3; i++) {
+            const double v0 = g[i], v1 = g[i] + g[3 + i], v2 = g[i] + g[6 + i];
+            it.lo[i] = std::min(v0, std::min(v1, v2));
+            it.hi[i] = std::max(v0, std::max(v1, v2));
+            l1 += g[3 + i] * g[3 + i];
+            l2 += g[6 + i] * g[6 + i];
+            l3 += (g[6 + i] - g[3 + i]) * (g[6 + i] - g[3 + i]);
+        }
+        const double L2 = std::max(l1, std::max(l2, l3));      // longest edge, squared
+        // Moller-Trumbore divides by det = e1 . (d x e2).  Its rounding error, relative to the
+        // barycentric margin a ray that misses the widened box has, is bounded by
+        // ~6*sqrt(3)*eps*L^2*scale / (delta * |e1 x e2| * |cos(theta)|): negligible unless the
+        // triangle is skinny (|e1 x e2| << L^2).  Skinny triangles (|e1 x e2| <= 1e-3 L^2) are
+        // never culled; DESIGN.md §5.1 has the bound.
+        const double cx = g[4] * g[8] - g[5] * g[7], cy = g[5] * g[6] - g[3] * g[8], cz = g[3] * g[7] - g[4] * g[6];
+        const double area2 = cx * cx + cy * cy + cz * cz;
+        if (!(area2 > 1e-6 * L2 * L2)) finite = false;
+    }
+    for (int i = 0; i < 3; i++) {
+        finite = finite && isfinite(it.lo[i]) && isfinite(it.hi[i]) && isfinite(g[i]);
+        it.c[i] = 0.5 * (it.lo[i] + it.hi[i]);
+    }
+    if (!finite) {
+        for (int i = 0; i < 3; i++) {
+            it.lo[i] = -INFINITY; it.hi[i] = INFINITY;
+            it.c[i] = isfinite(g[i]) ? g[i] : 0.0;
+        }
+        return;
+    }
+    for (int i = 0; i < 3; i++) { it.lo[i] -= delta; it.hi[i] += delta; }
+}
+
+struct Builder {
+    std::vector<RtBvh> *bvh;
+    std::vector<int> order;     // output slot order (indices into items)
+    std::vector<Item> *items;
+    int leaf;
+
+    void emit(int b, int e)     // items [b, e) of *items (already permuted in place)
+    {
+        const int me = (int)bvh->size();
+        bvh->push_back(RtBvh());
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int k = b; k < e; k++) {
+            const Item &it = (*items)[k];
+            for (int i = 0; i < 3; i++) {
+                lo[i] = std::min(lo[i], it.lo[i]); hi[i] = std::max(hi[i], it.hi[i]);
+                clo[i] = std::min(clo[i], it.c[i]); chi[i] = std::max(chi[i], it.c[i]);
+            }
+        }
+        RtBvh node;
+        for (int i = 0; i < 3; i++) { node.lo[i] = round_down(lo[i]); node.hi[i] = round_up(hi[i]); }
+        if (e - b <= leaf) {
+            node.info = ((int)order.size() << 4) | (e - b);
+            for (int k = b; k < e; k++) order.push_back(k);
+        } else {
+            int axis = 0;
+            double ext = -1;
+            for (int i = 0; i < 3; i++)
+                if (chi[i] - clo[i] > ext) { ext = chi[i] - clo[i]; axis = i; }
+            const int mid = b + (e - b) / 2;
+            std::nth_element(items->begin() + b, items->begin() + mid, items->begin() + e,
+                             [axis](const Item &x, const Item &y) {
+                                 return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.slot < y.slot);
+                             });
+            node.info = -1;
+            (*bvh)[me] = node;
+            emit(b, mid);
+            emit(mid, e);
+        }
+        node.skip = (int)bvh->size();
+        (*bvh)[me] = node;
+    }
+};
+
+}  // namespace
+
+// prim: all records in global list order (rank = index).  Rewrites `prim` into per-node cull
+// order, fills `bvh`, node_ent (4 ints per node) and the Set-order type prefix counts.
+int rt_build_cull(const rt_scene_desc *s, std::vector<RtPrim> &prim, std::vector<RtBvh> &bvh,
+                  std::vector<int32_t> &node_ent, std::vector<int32_t> &prefix, int leaf)
+{
+    const int N = s->n_nodes;
+    double scale = fabs(s->node_size[0]);
+    for (int i = 0; i < 3; i++)
+        scale = std::max(scale, std::max(fabs(s->node_pos[i]), fabs(s->node_pos[i] + s->node_size[0])));
+    const double delta = ldexp(scale, -13);          // ~1.2e-4 x scene scale
+    if (leaf < 1) leaf = 1;
+    if (leaf > 15) leaf = 15;
+    node_ent.assign(4 * (size_t)N, 0);
+    prefix.assign(4 * (size_t)(s->n_list ? s->n_list : 1), 0);
+    bvh.clear();
+    std::vector<RtPrim> out(prim.size());
+    std::vector<Item> items;
+    for (int n = 0; n < N; n++) {
+        const int b = s->node_ent_begin[n], c = s->node_ent_count[n];
+        int cnt[3] = {0, 0, 0};
+        for (int k = b; k < b + c; k++) {
+            cnt[prim[k].meta & 3]++;
+            for (int t = 0; t < 3; t++) prefix[4 * (size_t)k + t] = cnt[t];
+        }
+        node_ent[4 * n] = b;
+        node_ent[4 * n + 1] = c;
+        node_ent[4 * n + 2] = -1;
+        if (c == 0) continue;
+        items.resize(c);
+        for (int k = 0; k < c; k++) {
+            prim_bounds(prim[b + k], delta, items[k]);
+            items[k].slot = k;
+        }
+        const int root = (int)bvh.size();
+        Builder B{&bvh, {}, &items, leaf};
+        B.order.reserve(c);
+        B.emit(0, c);
+        const int end = (int)bvh.size();
+        for (int i = root; i < end; i++) {
+            if (bvh[i].skip >= end) bvh[i].skip = -1;
+            if (bvh[i].info >= 0) bvh[i].info = ((bvh[i].info >> 4) + b) << 4 | (bvh[i].info & 15);
+        }
+        for (int k = 0; k < c; k++) out[b + k] = prim[b + items[B.order[k]].slot];
+        node_ent[4 * n + 2] = root;
+    }
+    prim.swap(out);
+    return RT_OK;
+}

@@ -23,20 +23,34 @@ struct alignas(16) RtPrim {
                        // BOX:    pos.xyz, size
                        // FACE:   v0.xyz, e1.xyz, e2.xyz
     int32_t meta;      // type | shade << 2
-    int32_t entity;    // entity id (creation order)
+    int32_t rank;      // global list index k of this entity in its node's EntitySet order
 };
 static_assert(sizeof(RtPrim) == 80, "RtPrim must stay 80 bytes");
+
+// Per-node cull hierarchy: a binary BVH over one node's entity list, stored in
+// depth-first order with skip links (stackless).  Bounds are the entities' AABBs widened by a
+// margin and rounded outward to f32, so a ray that the exact binary64 test can report as hitting
+// an entity always passes its box.  Inner node: first child = this + 1.
+struct alignas(16) RtBvh {
+    float lo[3], hi[3];
+    int32_t skip;      // next node when this subtree is done or culled; -1 = end of this node's tree
+    int32_t info;      // leaf: first prim slot << 4 | count (1..15); inner: -1
+};
+static_assert(sizeof(RtBvh) == 32, "RtBvh must stay 32 bytes");
 
 struct RtDevScene {
     const double *node_ps;      // [n_nodes*4]
     const int32_t *node_child;  // [n_nodes*8]
     const int32_t *node_up;     // [n_nodes*2]
-    const int32_t *node_ent;    // [n_nodes*2]
-    const RtPrim *prim;         // [n_list]
+    const int32_t *node_ent;    // [n_nodes*4] {prim begin, count, bvh root (-1: none), 0}
+    const RtPrim *prim;         // [n_list] per node in cull-hierarchy leaf order
+    const RtBvh *bvh;           // [n_bvh]
+    const int32_t *list_entity; // [n_list] entity id per global list index (Set order)
+    const int32_t *list_prefix; // [n_list*4] per list index: #sph, #box, #tri in its node up to it (stats)
     const rt_shade *shades;     // [n_shades]
     const int32_t *ent_sub;     // [n_entities]
     const double *sub_ri;       // [n_substances]
-    int32_t n_nodes, n_list, n_entities, n_shades, n_subs, pad_;
+    int32_t n_nodes, n_list, n_entities, n_shades, n_subs, n_bvh;
 };
 
 // Per-frame state computed on the device by the setup kernel.
@@ -48,7 +62,8 @@ struct RtFrameSetup {
 };
 
 // Counter slots (rt_stats order).
-enum { CT_SEG, CT_RET, CT_SLOT, CT_LOC, CT_SPH, CT_BOX, CT_TRI, CT_HIT, CT_PRIM, CT_WARN, CT_FAULT, CT_N };
+enum { CT_SEG, CT_RET, CT_SLOT, CT_LOC, CT_SPH, CT_BOX, CT_TRI, CT_HIT, CT_PRIM, CT_WARN, CT_FAULT,
+       CT_CULL, CT_EXACT, CT_N };
 
 // Kernel launchers (rt_kernels.hip).
 struct RtLaunch {
@@ -66,6 +81,7 @@ struct RtLaunch {
     int32_t *fault;                             // device flag: some ray hit a reference throw
     int32_t blend;                              // col_weight != 1: read-modify-write rgb
     int32_t skip_trace;                         // ray generation only (rt_debug_camera_dirs)
+    int32_t cull;                               // use the per-node cull hierarchies
 };
 
 int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end);

@@ -116,7 +116,7 @@ struct Walker {
 };
 
 struct Counters {
-    long long ret, slot, loc, sph, box, tri, hit, steps;
+    long long ret, slot, loc, sph, box, tri, hit, steps, cull, exact;
 };
 
 // setup_cur_node — :251-278.  Returns 1/0 or -1 (throw).
@@ -351,6 +351,7 @@ __device__ __forceinline__ bool prim_within(const RtPrim &pr, const double p[3])
 }
 
 // entity_at_pos — src/octree_entity.ts:191-202.  Returns entity id, -1 undefined, -2 throw.
+// Prims of a node are stored in cull order, so the first entity in Set order is the minimum rank.
 __device__ int entity_at_pos(const RtDevScene &S, const double p[3], long long &levels)
 {
     int t = -1, oc = 0;
@@ -358,12 +359,101 @@ __device__ int entity_at_pos(const RtDevScene &S, const double p[3], long long &
     if (r < 0) return -2;
     int cur = r == 1 ? t : -1;
     while (cur >= 0) {
-        const int2 ent = reinterpret_cast<const int2 *>(S.node_ent)[cur];
+        const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[cur];
+        int best = 0x7fffffff;
         for (int k = ent.x; k < ent.x + ent.y; k++)
-            if (prim_within(S.prim[k], p)) return S.prim[k].entity;
+            if (S.prim[k].rank < best && prim_within(S.prim[k], p)) best = S.prim[k].rank;
+        if (best != 0x7fffffff) return S.list_entity[best];
         cur = reinterpret_cast<const int2 *>(S.node_up)[cur].x;
     }
     return -1;
+}
+
+// ---- per-node first collision (src/raytracer.ts:186-195) --------------------------------------------
+// Ray in f32 for the conservative box tests of the cull hierarchy.
+struct RayBox {
+    float ox, oy, oz, ix, iy, iz;
+    bool ok;           // finite ray: culling allowed
+};
+
+__device__ __forceinline__ float safe_inv(double d)
+{
+    const double dd = fabs(d) < 1e-30 ? copysign(1e-30, d) : d;
+    return 1.0f / (float)dd;
+}
+
+__device__ __forceinline__ RayBox make_raybox(const double o[3], const double d[3])
+{
+    RayBox rb;
+    rb.ox = (float)o[0]; rb.oy = (float)o[1]; rb.oz = (float)o[2];
+    rb.ix = safe_inv(d[0]); rb.iy = safe_inv(d[1]); rb.iz = safe_inv(d[2]);
+    rb.ok = isfinite(rb.ox) && isfinite(rb.oy) && isfinite(rb.oz) && fabs(d[0]) < 1e30 && fabs(d[1]) < 1e30 &&
+            fabs(d[2]) < 1e30 && !isnan(d[0]) && !isnan(d[1]) && !isnan(d[2]) && fabs(o[0]) < 1e30 &&
+            fabs(o[1]) < 1e30 && fabs(o[2]) < 1e30;
+    return rb;
+}
+
+// Does the half-line t >= 0 cross the box?  (slab test; fminf/fmaxf ignore NaN)
+__device__ __forceinline__ bool ray_box(const RtBvh &b, const RayBox &rb)
+{
+    const float tx0 = (b.lo[0] - rb.ox) * rb.ix, tx1 = (b.hi[0] - rb.ox) * rb.ix;
+    const float ty0 = (b.lo[1] - rb.oy) * rb.iy, ty1 = (b.hi[1] - rb.oy) * rb.iy;
+    const float tz0 = (b.lo[2] - rb.oz) * rb.iz, tz1 = (b.hi[2] - rb.oz) * rb.iz;
+    const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return tmin <= tmax;
+}
+
+// Entity.collision_info dispatch: 1 hit, 0 miss, -1 the reference throws.
+__device__ __forceinline__ int prim_hit(const RtPrim &pr, const double o[3], const double d[3], Hit &h)
+{
+    const int type = pr.meta & 3;
+    if (type == RT_ENT_FACE) return face_hit(pr.g, o, d, h) ? 1 : 0;
+    if (type == RT_ENT_SPHERE) return sphere_hit(pr.g, o, d, h) ? 1 : 0;
+    return box_hit(pr.g, o, d, h);
+}
+
+// The entity whose collision_info() the reference's Set-order loop stops at: the minimum rank among
+// exact hits (a throwing test counts as a hit: the loop reaches it only if nothing earlier hit).
+// Returns the prim slot or -1; *rank_out receives its rank.
+template <bool STATS>
+__device__ int node_first_hit(const RtDevScene &S, const int4 ne, const double o[3], const double d[3],
+                              const RayBox &rb, bool cull, Counters &c, Hit &h, int &rank_out)
+{
+    int best_rank = 0x7fffffff, best_slot = -1;
+    if (cull && rb.ok) {
+        int i = ne.z;
+        while (i >= 0) {
+            const RtBvh b = S.bvh[i];
+            c.cull++;
+            if (!ray_box(b, rb)) { i = b.skip; continue; }
+            if (b.info < 0) { i++; continue; }
+            const int first = b.info >> 4, n = b.info & 15;
+            for (int j = 0; j < n; j++) {
+                const int slot = first + j;
+                const int rk = S.prim[slot].rank;
+                if (rk >= best_rank) continue;
+                c.exact++;
+                if (prim_hit(S.prim[slot], o, d, h)) { best_rank = rk; best_slot = slot; }
+            }
+            i = b.skip;
+        }
+    } else {
+        for (int slot = ne.x; slot < ne.x + ne.y; slot++) {
+            const int rk = S.prim[slot].rank;
+            if (rk >= best_rank) continue;
+            c.exact++;
+            if (prim_hit(S.prim[slot], o, d, h)) { best_rank = rk; best_slot = slot; }
+        }
+    }
+    if (STATS && ne.y > 0) {
+        // tests the reference performs: Set order up to and including the first hit
+        const int k = best_slot >= 0 ? best_rank : ne.x + ne.y - 1;
+        const int4 pf = reinterpret_cast<const int4 *>(S.list_prefix)[k];
+        c.sph += pf.x; c.box += pf.y; c.tri += pf.z;
+    }
+    rank_out = best_rank;
+    return best_slot;
 }
 
 // ---- camera scan (src/view/camera.ts:207-250; vector.rotate_vectors src/math/vector.ts:318-323) ----
@@ -455,7 +545,8 @@ struct RayResult {
     int hit_ent, hit_node, segments, status;
 };
 
-__device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg,
+template <bool STATS>
+__device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg, bool cull,
                           const double cam_pos[3], const double dir0[3], RayResult &R, Counters &c)
 {
     double o[3] = {cam_pos[0], cam_pos[1], cam_pos[2]};
@@ -464,6 +555,7 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
     int refcount = 0, cur_sub = F.start_sub;
     bool light_hit = false;
     double path = 0;
+    RayBox rb = make_raybox(o, d);
     R.hit_ent = -1; R.hit_node = -1; R.segments = 1; R.status = ST_OK;
     Walker w;
     if (walker_set(S, w, o, d, F.start_tree >= 0, F.start_tree, F.start_oct, c) < 0) { R.status = ST_FAULT; goto done; }
@@ -472,26 +564,16 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         const int r = walker_next<false>(S, w, node, pt, po, c);
         if (r < 0) { R.status = r == -2 ? ST_CAP : ST_FAULT; goto done; }
         if (r == 0) break;
-        // for (entity of node.value.set): first collision wins
-        const int2 ent = reinterpret_cast<const int2 *>(S.node_ent)[node];
-        int hk = -1;
+        // for (entity of node.value.set): first collision in Set order wins
+        const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
+        if (ent.y == 0) continue;
         Hit h;
-        for (int k = ent.x; k < ent.x + ent.y; k++) {
-            const RtPrim &pr = S.prim[k];
-            const int type = pr.meta & 3;
-            int got;
-            if (type == RT_ENT_FACE) { c.tri++; got = face_hit(pr.g, o, d, h); }
-            else if (type == RT_ENT_SPHERE) { c.sph++; got = sphere_hit(pr.g, o, d, h); }
-            else { c.box++; got = box_hit(pr.g, o, d, h); }
-            if (got) {
-                if (got < 0) { R.status = ST_FAULT; goto done; }
-                hk = k;
-                break;
-            }
-        }
+        int rank;
+        const int hk = node_first_hit<STATS>(S, ent, o, d, rb, cull, c, h, rank);
         if (hk < 0) continue;
         const RtPrim &pr = S.prim[hk];
-        if (R.hit_ent < 0 && R.segments == 1) { R.hit_ent = pr.entity; R.hit_node = node; }
+        if (prim_hit(pr, o, d, h) < 0) { R.status = ST_FAULT; goto done; }   // recompute the winner's hit
+        if (R.hit_ent < 0 && R.segments == 1) { R.hit_ent = S.list_entity[rank]; R.hit_node = node; }
         if (dot3(d[0], d[1], d[2], h.n[0], h.n[1], h.n[2]) >= 0) { R.status = ST_WARN; goto done; }  // :200-203
         refcount++;
         c.hit++;
@@ -540,6 +622,7 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         if (walker_set(S, w, o, d, false, 0, 0, c) < 0) { R.status = ST_FAULT; goto done; }   // :254
         if (refcount >= cfg.refmax) { col0 = col1 = col2 = 0; goto done; }                 // COLOR_BLACK
         R.segments++;
+        rb = make_raybox(o, d);
     }
     if (!light_hit) {
         col0 = col0 * cfg.sky_rgb[0]; col1 = col1 * cfg.sky_rgb[1]; col2 = col2 * cfg.sky_rgb[2];
@@ -561,7 +644,7 @@ __global__ void __launch_bounds__(256) k_trace(RtLaunch L)
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     const bool active = x < W && lr < L.rows;
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     RayResult R;
     R.segments = 0; R.status = ST_OK;
     if (active) {
@@ -572,7 +655,7 @@ __global__ void __launch_bounds__(256) k_trace(RtLaunch L)
         if (F.fault) {
             R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.status = ST_FAULT;
         } else {
-            trace_ray(L.scene, F, L.cfg, L.cam.pos, dir0, R, c);
+            trace_ray<STATS>(L.scene, F, L.cfg, L.cull != 0, L.cam.pos, dir0, R, c);
         }
         // ExposureBuffer.set_color_i: c*w + old*(1-w), stored as f32 (src/view/exposure_buffer.ts:77-91)
         const double wgt = L.cfg.col_weight;
@@ -590,7 +673,8 @@ __global__ void __launch_bounds__(256) k_trace(RtLaunch L)
     }
     if (STATS) {
         long long v[CT_N] = {active ? R.segments : 0, c.ret, c.slot, c.loc, c.sph, c.box, c.tri, c.hit,
-                             active ? 1 : 0, R.status == ST_WARN, R.status == ST_FAULT || R.status == ST_CAP};
+                             active ? 1 : 0, R.status == ST_WARN, R.status == ST_FAULT || R.status == ST_CAP,
+                             c.cull, c.exact};
 #pragma unroll
         for (int k = 0; k < CT_N; k++) {
             const long long s = wave_sum(v[k]);
@@ -604,7 +688,7 @@ __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, doub
                              int max_out, int32_t *out_tree, int32_t *out_oct, int32_t *n_out)
 {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Walker w;
     const double o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz};
     int n = 0;

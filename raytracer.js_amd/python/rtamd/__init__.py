@@ -127,9 +127,9 @@ def build_scene(spec):
 class Context:
     """One rt_ctx bound to one GPU."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, flags=0):
         self.L = load_library()
-        cd = abi.rt_create_desc(device=int(device), flags=0)
+        cd = abi.rt_create_desc(device=int(device), flags=int(flags))
         h = C.c_void_p()
         _check(self.L.rt_create(C.byref(cd), C.byref(h)))
         self.h = h

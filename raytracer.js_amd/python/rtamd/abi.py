@@ -20,6 +20,7 @@ RT_ENT_SPHERE, RT_ENT_BOX, RT_ENT_FACE = 0, 1, 2
 RT_RESP_REFLECTION, RT_RESP_TRANSMISSION, RT_RESP_BOTH = 0, 1, 2
 
 STATUS_OK, STATUS_WARN, STATUS_FAULT, STATUS_CAP = 0, 1, 2, 3
+RT_CREATE_NO_CULL = 1
 
 _d = C.c_double
 _i = C.c_int32
@@ -60,13 +61,20 @@ class rt_stats(C.Structure):
     _fields_ = [("segments", C.c_int64), ("n_ret", C.c_int64), ("n_slot", C.c_int64),
                 ("n_loc", C.c_int64), ("n_sph", C.c_int64), ("n_box", C.c_int64),
                 ("n_tri", C.c_int64), ("n_hit", C.c_int64), ("primary", C.c_int64),
-                ("n_warn", C.c_int64), ("n_fault", C.c_int64), ("kernel_ms", _d), ("frame_ms", _d)]
+                ("n_warn", C.c_int64), ("n_fault", C.c_int64), ("n_cull", C.c_int64),
+                ("n_exact", C.c_int64), ("kernel_ms", _d), ("frame_ms", _d)]
 
+    # reference-equivalent work (compared with the oracle)
     COUNTERS = ("segments", "n_ret", "n_slot", "n_loc", "n_sph", "n_box", "n_tri", "n_hit",
                 "primary", "n_warn", "n_fault")
+    # work the GPU actually performed
+    WORK = ("n_cull", "n_exact")
 
     def counters(self):
         return {k: int(getattr(self, k)) for k in self.COUNTERS}
+
+    def work(self):
+        return {k: int(getattr(self, k)) for k in self.WORK}
 
 
 class rt_create_desc(C.Structure):

@@ -184,6 +184,29 @@ def test_transmission_scene(ctx):
     assert got["stats"].counters() == ref["counters"]
 
 
+@pytest.mark.parametrize("name", ["config1", "small6", "small8", "config2"])
+def test_cull_equals_exhaustive(ctx, name):
+    """The per-node cull hierarchies change work, not results: identical frames, ids, status and
+    reference-equivalent counters with RT_CREATE_NO_CULL (every entity tested exactly)."""
+    spec = {"config1": scenes.config1_spheres, "small6": lambda: scenes.small_random(6),
+            "small8": lambda: scenes.small_random(8, n_tri=800, half=0.05),
+            "config2": scenes.config2}[name]()
+    cam, cfg = scenes.make_camera(320, 200), scenes.make_config(3)
+    scene = rtamd.build_scene(spec)
+    ctx.upload(scene)
+    a = ctx.trace_frame(cam, cfg, allow_fault=True)
+    ex = rtamd.Context(0, flags=abi.RT_CREATE_NO_CULL)
+    try:
+        ex.upload(scene)
+        b = ex.trace_frame(cam, cfg, allow_fault=True)
+    finally:
+        ex.close()
+    for k in ("rgb", "hit_entity", "hit_node", "status"):
+        assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+    assert a["stats"].counters() == b["stats"].counters()
+    assert a["stats"].n_exact <= b["stats"].n_exact
+
+
 def test_roughness_rejected(ctx):
     spec = scenes.config1_spheres()
     sh = spec.shades.copy()
