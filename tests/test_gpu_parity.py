@@ -189,7 +189,7 @@ def test_cull_equals_exhaustive(ctx, name):
     """The per-node cull hierarchies change work, not results: identical frames, ids, status and
     reference-equivalent counters with RT_CREATE_NO_CULL (every entity tested exactly)."""
     spec = {"config1": scenes.config1_spheres, "small6": lambda: scenes.small_random(6),
-            "small8": lambda: scenes.small_random(8, n_tri=800, half=0.05),
+            "small8": lambda: scenes.small_random(8, n_tri=800, half=0.04),
             "config2": scenes.config2}[name]()
     cam, cfg = scenes.make_camera(320, 200), scenes.make_config(3)
     scene = rtamd.build_scene(spec)
