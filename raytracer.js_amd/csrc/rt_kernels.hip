@@ -107,6 +107,8 @@ enum : int { F_RET = 1, F_STEPPED = 2, F_AHEAD = 4 };
 
 struct Walker {
     double o[3], d[3];     // this.pos / this.direction
+    double inv[3];         // RN(1/d) per axis, for the slot-exit selection (see slot_exit)
+    bool fast;             // every d component is 0 or normal: the reciprocal shortcut is valid
     double np[3];          // next_pos[0]
     int nn;                // next_pos[1]: face index | negate << 3 | valid << 4
     int cur_tree;          // -1: cur_node undefined
@@ -160,7 +162,88 @@ __device__ int walker_set(const RtDevScene &S, Walker &w, const double o[3], con
         else { w.cur_tree = -1; w.cur_oct = RT_OCT_UNDEF; }
     }
     w.o[0] = o[0]; w.o[1] = o[1]; w.o[2] = o[2];
+    bool fast = true;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        w.inv[a] = 1.0 / d[a];
+        // a subnormal component makes RN(1/d) overflow; a huge one underflows it
+        fast = fast && (d[a] == 0.0 || (fabs(d[a]) >= 2.2250738585072014e-308 && fabs(d[a]) <= 1e300) || isnan(d[a]));
+    }
+    w.fast = fast;
     return walker_setup(S, w) < 0 ? -1 : 0;
+}
+
+// The exit half of Box.line_intersection (src/math/intersection.ts:150-204) for a walker slot:
+// u2 = the first minimum over exit faces of q/p and the emptiness check u1 > u2, bit-identical to
+// six IEEE divisions.  Exactly one face per axis is an exit face (isNegative(p) selects entering),
+// so three exit and three entry quotients exist.  Each is first approximated by q * RN(1/d),
+// which is within 3 ulps of RN(q/d) (relative error <= 3 eps for normal d; exact for d = +-0
+// where both are +-inf or NaN).  Any candidate farther than 8 ulps from the minimum cannot be
+// (or tie with) the exact minimum, so only the survivors are divided exactly — normally one.
+// Returns false for the reference's [] (then update_next_pos throws).
+__device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, double size, const Walker &w,
+                                          double &u2o, int &i2o)
+{
+    const double hs = size * 0.5;
+    const double c[3] = {cx, cy, cz};
+    double qe[3], pe[3], ae[3], qn[3], pn[3], an[3];
+    int fe[3];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double tl = c[a] - hs;
+        const double qlo = w.o[a] - tl;
+        const double qhi = tl + size - w.o[a];
+        // face 2a: p = -d, face 2a+1: p = d; isNegative(p) picks the entering one
+        const bool neg = signbit(w.d[a]);
+        qe[a] = neg ? qlo : qhi;   pe[a] = neg ? -w.d[a] : w.d[a];   fe[a] = neg ? 2 * a : 2 * a + 1;
+        qn[a] = neg ? qhi : qlo;   pn[a] = neg ? w.d[a] : -w.d[a];
+        ae[a] = qe[a] * (neg ? -w.inv[a] : w.inv[a]);
+        an[a] = qn[a] * (neg ? w.inv[a] : -w.inv[a]);
+    }
+    // exit: the reference keeps the first strict minimum over faces in order (u2 starts at +inf)
+    double m = INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; a++) m = ae[a] < m ? ae[a] : m;
+    double u2 = INFINITY;
+    int i2 = -1;
+    if (m < INFINITY) {
+        const double tol = fabs(m) * 1.7763568394002505e-15 + 1e-300;   // 8 eps |m| + subnormal slack
+        if (!(fabs(m) < 1e300)) {
+            // out of the shortcut's range: exact for every axis
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const double e = qe[a] / pe[a];
+                if (e < u2) { u2 = e; i2 = fe[a]; }
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                if (ae[a] <= m + tol) {                   // survivor (NaN never survives)
+                    const double e = qe[a] / pe[a];
+                    if (e < u2) { u2 = e; i2 = fe[a]; }
+                }
+            }
+        }
+    }
+    // entry: u1 = first strict maximum (starts at -inf); only `u1 > u2` matters
+    double M = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; a++) M = an[a] > M ? an[a] : M;
+    if (M > -INFINITY) {
+        const double tolM = fabs(M) * 1.7763568394002505e-15 + 1e-300;
+        if (!(M + tolM < u2) || !(fabs(M) < 1e300)) {
+            double u1 = -INFINITY;
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const double e = qn[a] / pn[a];
+                if (e > u1) u1 = e;
+            }
+            if (u1 > u2) return false;
+        }
+    }
+    u2o = u2;
+    i2o = i2;
+    return true;
 }
 
 // update_next_pos — :369-384 with dim_relative_to_parent :127-136.  Returns 0 or -1 (throw).
@@ -173,12 +256,20 @@ __device__ __forceinline__ int walker_update_next_pos(const RtDevScene &S, Walke
     const double dx = p.x + (double)((n >> 0) & 1) * ph;
     const double dy = p.y + (double)((n >> 1) & 1) * ph;
     const double dz = p.z + (double)((n >> 2) & 1) * ph;
-    BoxIsect bi;
-    if (!box_isect(dx + 0.5 * ph, dy + 0.5 * ph, dz + 0.5 * ph, 1 * ph, w.o, w.d, bi)) return -1;
-    w.np[0] = w.o[0] + w.d[0] * bi.u2;
-    w.np[1] = w.o[1] + w.d[1] * bi.u2;
-    w.np[2] = w.o[2] + w.d[2] * bi.u2;
-    w.nn = bi.i2 >= 0 ? (bi.i2 | 16) : 0;
+    double u2;
+    int i2;
+    if (w.fast) {
+        if (!slot_exit(dx + 0.5 * ph, dy + 0.5 * ph, dz + 0.5 * ph, 1 * ph, w, u2, i2)) return -1;
+    } else {
+        BoxIsect bi;
+        if (!box_isect(dx + 0.5 * ph, dy + 0.5 * ph, dz + 0.5 * ph, 1 * ph, w.o, w.d, bi)) return -1;
+        u2 = bi.u2;
+        i2 = bi.i2;
+    }
+    w.np[0] = w.o[0] + w.d[0] * u2;
+    w.np[1] = w.o[1] + w.d[1] * u2;
+    w.np[2] = w.o[2] + w.d[2] * u2;
+    w.nn = i2 >= 0 ? (i2 | 16) : 0;
     return 0;
 }
 

@@ -180,7 +180,8 @@ def config3():
 def small_random(seed, n_tri=200, n_sph=40, n_box=10, depth=5, p_mirror=0.3, p_light=0.1, half=0.02):
     """Small mixed scenes for parity sweeps (all three primitive kinds, mirrors, lights)."""
     st = Stream(seed)
-    tri = random_triangles(st, n_tri, half, lo=0.05, hi=0.95, max_in_depth=depth)
+    # a triangle's cubic AABB is [min corner, min corner + max extent]: keep centre + 3*half inside
+    tri = random_triangles(st, n_tri, half, lo=half + 0.01, hi=1 - 3 * half - 0.01, max_in_depth=depth)
     sph = random_spheres(st, n_sph, 0.01, 0.12, lo=0.15, hi=0.85, max_in_depth=depth)
     box = _entities(n_box)
     box["type"] = abi.RT_ENT_BOX

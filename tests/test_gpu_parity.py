@@ -108,6 +108,35 @@ def test_walker_matches_oracle_random_rays(ctx):
             assert got == ref
 
 
+def test_walker_special_directions(ctx):
+    """Slot-exit shortcut (q * RN(1/d) screening, exact division for survivors) against the
+    oracle's six IEEE divisions: directions with +-0, subnormal, tiny and huge components, dyadic
+    origins on node boundaries (exact ties between exit faces)."""
+    spec = scenes.small_random(9, n_tri=400, depth=6)
+    ctx.upload(rtamd.build_scene(spec))
+    w, root = oracle.build_scene(spec)
+    w.linearize(root)
+    rng = np.random.default_rng(11)
+    specials = [0.0, -0.0, 5e-324, -5e-324, 1e-310, 1e-200, -1e-30, 1.0, -1.0, 0.5, 1e300, 3.0]
+    wk = w.walker(root, include_undefined=True)
+    n = 0
+    for _ in range(400):
+        o = rng.integers(0, 65, 3) / 64.0 if rng.random() < 0.5 else rng.uniform(0, 1, 3)
+        d = rng.normal(size=3)
+        for a in range(3):
+            if rng.random() < 0.35:
+                d[a] = specials[rng.integers(len(specials))]
+        try:
+            ref = [(w.tree_id(pt), -1 if po is None else po) for _, pt, po in w.walk(wk, o.tolist(), d.tolist())]
+        except RuntimeError:
+            with pytest.raises(rtamd.RtError):
+                ctx.debug_walk(o.tolist(), d.tolist(), include_undefined=True)
+            continue
+        assert ctx.debug_walk(o.tolist(), d.tolist(), include_undefined=True) == ref, (o, d)
+        n += 1
+    assert n > 200
+
+
 # ---- ray generation --------------------------------------------------------------------------------------
 @pytest.mark.parametrize("wh", [(256, 256), (1920, 1080), (101, 37), (2, 1)])
 def test_camera_dirs_bit_exact(ctx, wh):
