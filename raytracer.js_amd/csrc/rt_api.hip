@@ -72,6 +72,8 @@ struct rt_ctx {
     int device = 0;
     int flags = 0;
     int bvh_leaf = 4;
+    int occ = 0;
+    int diag = 0;
     hipStream_t stream = nullptr;
     bool has_scene = false;
     bool scatter = false;            // a mirror shade with roughness > 0 is reachable
@@ -106,6 +108,8 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_NO_CULL"))
         if (e[0] == '1') c->flags |= RT_CREATE_NO_CULL;
     if (const char *e = getenv("RT_BVH_LEAF")) c->bvh_leaf = atoi(e);
+    if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
+    if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     int r = use_device(c);
     if (r == RT_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         r = rt_set_error(RT_E_HIP, "rt_create: hipStreamCreate failed");
@@ -314,6 +318,8 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.status = want_ids ? (uint8_t *)c->b_status.p : nullptr;
     L.fault = (int32_t *)c->b_fault.p;
     L.cull = (c->flags & RT_CREATE_NO_CULL) ? 0 : 1;
+    L.occ = c->occ;
+    L.diag = c->diag;
     return RT_OK;
 }
 

@@ -82,6 +82,8 @@ struct RtLaunch {
     int32_t blend;                              // col_weight != 1: read-modify-write rgb
     int32_t skip_trace;                         // ray generation only (rt_debug_camera_dirs)
     int32_t cull;                               // use the per-node cull hierarchies
+    int32_t occ;                                // k_trace occupancy variant (RT_OCC; 0 = default)
+    int32_t diag;                               // RT_DIAG bits (timing experiments only; wrong images)
 };
 
 int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end);

@@ -638,7 +638,7 @@ struct RayResult {
 
 template <bool STATS>
 __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg, bool cull,
-                          const double cam_pos[3], const double dir0[3], RayResult &R, Counters &c)
+                          int diag, const double cam_pos[3], const double dir0[3], RayResult &R, Counters &c)
 {
     double o[3] = {cam_pos[0], cam_pos[1], cam_pos[2]};
     double d[3] = {dir0[0], dir0[1], dir0[2]};
@@ -657,7 +657,7 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         if (r == 0) break;
         // for (entity of node.value.set): first collision in Set order wins
         const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
-        if (ent.y == 0) continue;
+        if (ent.y == 0 || (diag & 1)) continue;        // diag bit 0: walker-only timing
         Hit h;
         int rank;
         const int hk = node_first_hit<STATS>(S, ent, o, d, rb, cull, c, h, rank);
@@ -727,8 +727,8 @@ done:
 }
 
 // One lane per pixel of this part; 256-lane blocks cover 16x16 pixel tiles, each wave an 8x8 tile.
-template <bool STATS>
-__global__ void __launch_bounds__(256) k_trace(RtLaunch L)
+template <bool STATS, int MINW>
+__global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
 {
     const int W = L.cam.width;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -746,7 +746,7 @@ __global__ void __launch_bounds__(256) k_trace(RtLaunch L)
         if (F.fault) {
             R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.status = ST_FAULT;
         } else {
-            trace_ray<STATS>(L.scene, F, L.cfg, L.cull != 0, L.cam.pos, dir0, R, c);
+            trace_ray<STATS>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, dir0, R, c);
         }
         // ExposureBuffer.set_color_i: c*w + old*(1-w), stored as f32 (src/view/exposure_buffer.ts:77-91)
         const double wgt = L.cfg.col_weight;
@@ -819,8 +819,12 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     if (L.skip_trace) return RT_OK;
     const dim3 grid((W + 15) / 16, (L.rows + 15) / 16);
     if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
-    if (L.counters) hipLaunchKernelGGL(k_trace<true>, grid, dim3(256), 0, st, L);
-    else hipLaunchKernelGGL(k_trace<false>, grid, dim3(256), 0, st, L);
+    // occupancy variants (waves per SIMD the register allocation must admit); RT_OCC selects
+    if (L.counters) hipLaunchKernelGGL((k_trace<true, 1>), grid, dim3(256), 0, st, L);
+    else if (L.occ == 4) hipLaunchKernelGGL((k_trace<false, 4>), grid, dim3(256), 0, st, L);
+    else if (L.occ == 5) hipLaunchKernelGGL((k_trace<false, 5>), grid, dim3(256), 0, st, L);
+    else if (L.occ == 6) hipLaunchKernelGGL((k_trace<false, 6>), grid, dim3(256), 0, st, L);
+    else hipLaunchKernelGGL((k_trace<false, 1>), grid, dim3(256), 0, st, L);
     HIP_TRY(hipGetLastError());
     if (ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
     return RT_OK;
