@@ -71,7 +71,7 @@ int rt_build_cull(const rt_scene_desc *s, std::vector<RtPrim> &prim, std::vector
 struct rt_ctx {
     int device = 0;
     int flags = 0;
-    int bvh_leaf = 4;
+    int bvh_leaf = 2;
     int occ = 0;
     int diag = 0;
     hipStream_t stream = nullptr;
@@ -118,7 +118,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
             r = rt_set_error(RT_E_HIP, "rt_create: hipEventCreate failed");
     if (r == RT_OK) r = c->b_setup.ensure(sizeof(RtFrameSetup));
     if (r == RT_OK) r = c->b_counters.ensure(sizeof(unsigned long long) * CT_N);
-    if (r == RT_OK) r = c->b_fault.ensure(sizeof(int));
+    if (r == RT_OK) r = c->b_fault.ensure(4 * sizeof(int));   // [0] fault flag, [1] tile queue head
     if (r != RT_OK) {
         rt_destroy(c);
         return r;
@@ -318,6 +318,7 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.status = want_ids ? (uint8_t *)c->b_status.p : nullptr;
     L.fault = (int32_t *)c->b_fault.p;
     L.cull = (c->flags & RT_CREATE_NO_CULL) ? 0 : 1;
+    L.tile_counter = (int32_t *)c->b_fault.p + 1;
     L.occ = c->occ;
     L.diag = c->diag;
     return RT_OK;

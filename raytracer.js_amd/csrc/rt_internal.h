@@ -79,6 +79,7 @@ struct RtLaunch {
     uint8_t *status;                            // device [rows*W] or null
     unsigned long long *counters;               // device [CT_N] or null (stats build)
     int32_t *fault;                             // device flag: some ray hit a reference throw
+    int32_t *tile_counter;                      // device work queue head (zeroed per launch)
     int32_t blend;                              // col_weight != 1: read-modify-write rgb
     int32_t skip_trace;                         // ray generation only (rt_debug_camera_dirs)
     int32_t cull;                               // use the per-node cull hierarchies

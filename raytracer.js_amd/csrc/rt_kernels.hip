@@ -727,24 +727,35 @@ done:
 }
 
 // One lane per pixel of this part; 256-lane blocks cover 16x16 pixel tiles, each wave an 8x8 tile.
+// Persistent waves: each wave repeatedly takes the next 8x8 pixel tile from an atomic queue
+// (one returning atomic per tile, lane 0) and traces it one ray per lane.  Per-ray cost varies by
+// orders of magnitude across the frame (rays that hit early vs rays that cross every upper-level
+// set), so wave-granular dynamic scheduling replaces the fixed block->tile mapping and its tail.
 template <bool STATS, int MINW>
 __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
 {
     const int W = L.cam.width;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool active = x < W && lr < L.rows;
+    const int lane = threadIdx.x & 63;
+    const int tiles_x = (W + 7) >> 3;
+    const int n_tiles = tiles_x * ((L.rows + 7) >> 3);
+    const RtFrameSetup F = *L.setup;
+    const size_t plane = (size_t)L.rows * (size_t)W;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    RayResult R;
-    R.segments = 0; R.status = ST_OK;
-    if (active) {
-        const RtFrameSetup F = *L.setup;
+    long long n_seg = 0, n_prim = 0, n_warn = 0, n_fault = 0;
+    for (;;) {
+        int t = 0;
+        if (lane == 0) t = atomicAdd(L.tile_counter, 1);
+        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+        if (t >= n_tiles) break;
+        const int ty = t / tiles_x, tx = t - ty * tiles_x;
+        const int x = tx * 8 + (lane & 7);
+        const int lr = ty * 8 + (lane >> 3);
+        if (x >= W || lr >= L.rows) continue;
+        RayResult R;
         const size_t pix = (size_t)lr * (size_t)W + (size_t)x;
-        const size_t plane = (size_t)L.rows * (size_t)W;
         const double dir0[3] = {L.dirs[pix], L.dirs[plane + pix], L.dirs[2 * plane + pix]};
         if (F.fault) {
-            R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.status = ST_FAULT;
+            R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.segments = 1; R.status = ST_FAULT;
         } else {
             trace_ray<STATS>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, dir0, R, c);
         }
@@ -761,11 +772,16 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
         if (L.hit_node) L.hit_node[pix] = R.hit_node;
         if (L.status) L.status[pix] = (uint8_t)R.status;
         if (R.status >= ST_FAULT && L.fault) atomicOr(L.fault, 1);
+        if (STATS) {
+            n_seg += R.segments;
+            n_prim += 1;
+            n_warn += R.status == ST_WARN;
+            n_fault += R.status == ST_FAULT || R.status == ST_CAP;
+        }
     }
     if (STATS) {
-        long long v[CT_N] = {active ? R.segments : 0, c.ret, c.slot, c.loc, c.sph, c.box, c.tri, c.hit,
-                             active ? 1 : 0, R.status == ST_WARN, R.status == ST_FAULT || R.status == ST_CAP,
-                             c.cull, c.exact};
+        long long v[CT_N] = {n_seg, c.ret, c.slot, c.loc, c.sph, c.box, c.tri, c.hit,
+                             n_prim, n_warn, n_fault, c.cull, c.exact};
 #pragma unroll
         for (int k = 0; k < CT_N; k++) {
             const long long s = wave_sum(v[k]);
@@ -805,6 +821,24 @@ __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, doub
         if (e_ != hipSuccess) return rt_set_error(RT_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
     } while (0)
 
+// Persistent grid: every CU filled to the occupancy the kernel's registers admit.  The tile queue
+// makes an over-estimate harmless (late blocks find the queue empty).
+static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const RtLaunch &L)
+{
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus < 1) cus = 1;
+    }
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void *>(kernel), 256, 0) != hipSuccess ||
+        per < 1)
+        per = 1;
+    hipLaunchKernelGGL(kernel, dim3(cus * per), dim3(256), 0, st, L);
+}
+
 int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end)
 {
     hipStream_t st = (hipStream_t)stream;
@@ -817,14 +851,15 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
                        L.stripe_rows, L.rows, (const double *)L.fr_rows, L.dirs);
     HIP_TRY(hipGetLastError());
     if (L.skip_trace) return RT_OK;
-    const dim3 grid((W + 15) / 16, (L.rows + 15) / 16);
+    (void)W;
+    HIP_TRY(hipMemsetAsync(L.tile_counter, 0, sizeof(int32_t), st));
     if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
     // occupancy variants (waves per SIMD the register allocation must admit); RT_OCC selects
-    if (L.counters) hipLaunchKernelGGL((k_trace<true, 1>), grid, dim3(256), 0, st, L);
-    else if (L.occ == 4) hipLaunchKernelGGL((k_trace<false, 4>), grid, dim3(256), 0, st, L);
-    else if (L.occ == 5) hipLaunchKernelGGL((k_trace<false, 5>), grid, dim3(256), 0, st, L);
-    else if (L.occ == 6) hipLaunchKernelGGL((k_trace<false, 6>), grid, dim3(256), 0, st, L);
-    else hipLaunchKernelGGL((k_trace<false, 1>), grid, dim3(256), 0, st, L);
+    if (L.counters) launch_persistent(k_trace<true, 2>, st, L);
+    else if (L.occ == 2) launch_persistent(k_trace<false, 2>, st, L);
+    else if (L.occ == 4) launch_persistent(k_trace<false, 4>, st, L);
+    else if (L.occ == 5) launch_persistent(k_trace<false, 5>, st, L);
+    else launch_persistent(k_trace<false, 3>, st, L);
     HIP_TRY(hipGetLastError());
     if (ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
     return RT_OK;
