@@ -71,7 +71,7 @@ int rt_build_cull(const rt_scene_desc *s, std::vector<RtPrim> &prim, std::vector
 struct rt_ctx {
     int device = 0;
     int flags = 0;
-    int bvh_leaf = 2;
+    int bvh_leaf = 1;                // cull-hierarchy leaf size (RT_BVH_LEAF); 1 measured fastest
     int occ = 0;
     int diag = 0;
     hipStream_t stream = nullptr;
@@ -476,6 +476,9 @@ extern "C" int rt_debug_camera_dirs(rt_ctx *c, const rt_camera_desc *cam, double
     HIP_TRY(hipMemcpyAsync(soa.data(), L.dirs, sizeof(double) * 3 * P, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (size_t p = 0; p < P; p++)
-        for (int i = 0; i < 3; i++) dirs_out[3 * p + i] = soa[i * P + p];
+        for (int i = 0; i < 3; i++) {
+            const size_t x = p % (size_t)cam->width, y = p / (size_t)cam->width;
+            dirs_out[3 * p + i] = soa[i * P + x * (size_t)cam->height + y];   // x-major on the device
+        }
     return RT_OK;
 }

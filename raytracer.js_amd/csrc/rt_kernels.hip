@@ -509,14 +509,14 @@ __device__ __forceinline__ int prim_hit(const RtPrim &pr, const double o[3], con
 // Returns the prim slot or -1; *rank_out receives its rank.
 template <bool STATS>
 __device__ int node_first_hit(const RtDevScene &S, const int4 ne, const double o[3], const double d[3],
-                              const RayBox &rb, bool cull, Counters &c, Hit &h, int &rank_out)
+                              const RayBox &rb, bool cull, Counters &c, long long &box_ctr, Hit &h, int &rank_out)
 {
     int best_rank = 0x7fffffff, best_slot = -1;
     if (cull && rb.ok) {
         int i = ne.z;
         while (i >= 0) {
             const RtBvh b = S.bvh[i];
-            c.cull++;
+            box_ctr++;
             if (!ray_box(b, rb)) { i = b.skip; continue; }
             if (b.info < 0) { i++; continue; }
             const int first = b.info >> 4, n = b.info & 15;
@@ -565,11 +565,46 @@ __device__ __forceinline__ int part_row_to_y(int lr, int part, int n_parts, int 
 }
 
 // ---- kernels -------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_frame_setup(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
-                                                    RtFrameSetup *setup, double *fr_rows)
+__device__ __forceinline__ int wave_min(int v)
 {
-    const int lane = threadIdx.x;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// Two waves: wave 0 runs the two vertical scan chains (lanes 0/1); wave 1 locates the camera
+// (node_at_pos) and finds its substance with a wave-cooperative entity_at_pos (64 entities per
+// step, minimum Set rank among is_within hits).
+__global__ void __launch_bounds__(128) k_frame_setup(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
+                                                     RtFrameSetup *setup, double *fr_rows)
+{
+    const int lane = threadIdx.x & 63;
     const int H = cam.height;
+    if (threadIdx.x >= 64) {
+        long long lv = 0;
+        int t = -1, oc = 0;
+        const int r = node_at_pos(S, cam.pos, t, oc, lv);
+        int se = -1;
+        int cur = r == 1 ? t : -1;
+        while (cur >= 0) {
+            const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[cur];
+            int best = 0x7fffffff;
+            for (int k = ent.x + lane; k < ent.x + ent.y; k += 64)
+                if (S.prim[k].rank < best && prim_within(S.prim[k], cam.pos)) best = S.prim[k].rank;
+            best = wave_min(best);
+            if (best != 0x7fffffff) { se = S.list_entity[best]; break; }
+            cur = reinterpret_cast<const int2 *>(S.node_up)[cur].x;
+        }
+        if (lane == 0) {
+            RtFrameSetup f;
+            f.fault = r < 0;
+            f.start_tree = r == 1 ? t : -1;
+            f.start_oct = oc;
+            f.start_sub = se >= 0 ? S.ent_sub[se] : cfg.default_substance;
+            *setup = f;
+        }
+        return;
+    }
     if (lane == 0 || lane == 1) {
         // iter_v(H>>1, H, rot_scan_v_v, 1, false) / iter_v((H>>1)-1, -1, counter, -1, true)
         const bool top = lane == 0;
@@ -583,28 +618,20 @@ __global__ void __launch_bounds__(64) k_frame_setup(RtDevScene S, rt_camera_desc
             fr_rows[3 * y + 2] = fr[2];
             rotate_pair(fr, up, c, s);
         }
-    } else if (lane == 2) {
-        long long lv = 0;
-        int t = -1, oc = 0;
-        const int r = node_at_pos(S, cam.pos, t, oc, lv);
-        const int se = entity_at_pos(S, cam.pos, lv);
-        RtFrameSetup f;
-        f.fault = (r < 0 || se == -2);
-        f.start_tree = r == 1 ? t : -1;
-        f.start_oct = oc;
-        f.start_sub = se >= 0 ? S.ent_sub[se] : cfg.default_substance;
-        *setup = f;
     }
 }
 
-// One lane per (row of this part, half).  dirs: SoA planes [3][rows*W].
+// One lane per (half, row of this part): lanes [0, rows) run the right half-rows, [rows, 2 rows)
+// the left ones, so at every chain step a wave stores 64 consecutive rows of one column.
+// dirs: SoA planes [3][W*rows], x-major (index x*rows + local row): coalesced stores here, and
+// an 8x8 tile of k_trace reads 8 runs of 64 bytes per plane.
 __global__ void __launch_bounds__(256) k_raygen(rt_camera_desc cam, int part, int n_parts, int stripe, int rows,
                                                 const double *__restrict__ fr_rows, double *__restrict__ dirs)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= 2 * rows) return;
-    const int lr = t >> 1;
-    const bool right = (t & 1) == 0;
+    const bool right = t < rows;
+    const int lr = right ? t : t - rows;
     const int W = cam.width;
     const int y = part_row_to_y(lr, part, n_parts, stripe);
     // iter_h(W>>1, W, y, rot_scan_h_v, fr_v, 1, false) / iter_h((W>>1)-1, -1, y, counter, fr_v, -1, true)
@@ -614,11 +641,11 @@ __global__ void __launch_bounds__(256) k_raygen(rt_camera_desc cam, int part, in
     if (!right) rotate_pair(f, l, c, s);
     const int from = right ? (W >> 1) : (W >> 1) - 1, to = right ? W : -1, inc = right ? 1 : -1;
     const size_t plane = (size_t)rows * (size_t)W;
-    double *row = dirs + (size_t)lr * (size_t)W;
     for (int x = from; x != to; x += inc) {
-        row[x] = f[0];
-        row[plane + x] = f[1];
-        row[2 * plane + x] = f[2];
+        const size_t i = (size_t)x * (size_t)rows + (size_t)lr;
+        dirs[i] = f[0];
+        dirs[plane + i] = f[1];
+        dirs[2 * plane + i] = f[2];
         rotate_pair(f, l, c, s);
     }
 }
@@ -660,7 +687,14 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         if (ent.y == 0 || (diag & 1)) continue;        // diag bit 0: walker-only timing
         Hit h;
         int rank;
-        const int hk = node_first_hit<STATS>(S, ent, o, d, rb, cull, c, h, rank);
+        long long *box_ctr = &c.cull;
+        long long dummy = 0;
+        if (STATS && (diag & 2)) {
+            // diag bit 1 (stats only): n_cull counts box tests of octree levels 0-1, n_exact of 2-3
+            const double lvl = log2(S.node_ps[0 * 4 + 3] / S.node_ps[4 * node + 3]);
+            box_ctr = lvl < 1.5 ? &c.cull : (lvl < 3.5 ? &c.exact : &dummy);
+        }
+        const int hk = node_first_hit<STATS>(S, ent, o, d, rb, cull, c, *box_ctr, h, rank);
         if (hk < 0) continue;
         const RtPrim &pr = S.prim[hk];
         if (prim_hit(pr, o, d, h) < 0) { R.status = ST_FAULT; goto done; }   // recompute the winner's hit
@@ -753,7 +787,8 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
         if (x >= W || lr >= L.rows) continue;
         RayResult R;
         const size_t pix = (size_t)lr * (size_t)W + (size_t)x;
-        const double dir0[3] = {L.dirs[pix], L.dirs[plane + pix], L.dirs[2 * plane + pix]};
+        const size_t di = (size_t)x * (size_t)L.rows + (size_t)lr;           // x-major (k_raygen)
+        const double dir0[3] = {L.dirs[di], L.dirs[plane + di], L.dirs[2 * plane + di]};
         if (F.fault) {
             R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.segments = 1; R.status = ST_FAULT;
         } else {
@@ -843,7 +878,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
 {
     hipStream_t st = (hipStream_t)stream;
     const int W = L.cam.width;
-    hipLaunchKernelGGL(k_frame_setup, dim3(1), dim3(64), 0, st, L.scene, L.cam, L.cfg, L.setup, L.fr_rows);
+    hipLaunchKernelGGL(k_frame_setup, dim3(1), dim3(128), 0, st, L.scene, L.cam, L.cfg, L.setup, L.fr_rows);
     HIP_TRY(hipGetLastError());
     if (L.rows <= 0) return RT_OK;
     const int rg_threads = 2 * L.rows;
