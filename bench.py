@@ -13,9 +13,14 @@ HIP-event-timed kernel duration) and `cpu_baseline` (the oracle restatement, sin
 bounded pixel sample of the same workload).
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -27,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "raytracer.js_amd", "python"))
 
 import rtamd  # noqa: E402  (after torch: share its HIP runtime)
 from rtamd import scenes  # noqa: E402
+from rtamd.stripes import StripeGather  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # Algorithmic bytes per unit of work of the reference's algorithm (canonical f64
@@ -65,6 +71,68 @@ def cpu_baseline(spec, cam, cfg, budget_s):
                        % (done, cam.width, cam.height, segs, t_used))
 
 
+def _pmc_pass(counter, config, stripe, timeout_s):
+    """One rocprofv3 --pmc pass over a child bench run; mean counter value per k_trace<false,*> launch."""
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not on PATH"
+    out = tempfile.mkdtemp(prefix="rt_pmc_")
+    try:
+        env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+        cmd = [prof, "--pmc", counter, "-d", out, "-o", "pmc", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", config,
+               "--stripe", str(stripe), "--steps", "3", "--warmup", "1"]
+        r = subprocess.run(cmd, env=env, timeout=timeout_s, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        if r.returncode != 0:
+            tail = r.stdout.decode(errors="replace").strip().splitlines()[-3:]
+            return None, "%s pass exit %d: %s" % (counter, r.returncode, " | ".join(tail))
+        vals = []
+        for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    # the frame kernel only (the STATS instantiation is k_trace<true, ...>)
+                    name = r["Kernel_Name"]
+                    stats = "<true" in name or "ILb1E" in name
+                    if "k_trace" in name and not stats and r["Counter_Name"] == counter:
+                        vals.append(float(r["Counter_Value"]))
+        if not vals:
+            return None, "%s pass: no k_trace rows in the counter CSV" % counter
+        return sum(vals) / len(vals), None
+    except Exception as e:  # the bench line must not depend on the profiler
+        return None, "%s pass: %r" % (counter, e)
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
+def hbm_traffic(config, stripe, timeout_s=300):
+    """HBM bytes per k_trace launch from PMC (MI355X_MICROARCH.md HBM section): FETCH_SIZE and
+    WRITE_SIZE in separate passes (TCC slots), both in KiB; FETCH_SIZE doubled (gfx950 tallies
+    128-B requests at 64 B).  None when rocprofv3 or a pass is unavailable."""
+    fetch, err = _pmc_pass("FETCH_SIZE", config, stripe, timeout_s)
+    if err:
+        return None, err
+    write, err = _pmc_pass("WRITE_SIZE", config, stripe, timeout_s)
+    if err:
+        return None, err
+    return dict(bytes=2 * fetch * 1024 + write * 1024, fetch_kib_raw=fetch, write_kib=write,
+                method="rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes), per k_trace launch: "
+                       "2*FETCH_SIZE + WRITE_SIZE"), None
+
+
+def pmc_child(args):
+    """Minimal frame loop profiled by hbm_traffic(): no stats launch, no CPU baseline, no output."""
+    factory, W, H, refmax = scenes.WORKLOADS[args.config]
+    ctx = rtamd.Context(0)
+    ctx.upload(rtamd.build_scene(factory()))
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
+    buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
+    s = torch.cuda.Stream()
+    for _ in range(args.warmup + args.steps):
+        ctx.trace_rows_device(cam, cfg, 0, 1, args.stripe, buf.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -73,7 +141,11 @@ def main():
     ap.add_argument("--config", default="config3", choices=sorted(scenes.WORKLOADS))
     ap.add_argument("--stripe", type=int, default=8, help="rows per stripe of the row-interleaved split")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.pmc_child:
+        return pmc_child(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -97,29 +169,12 @@ def main():
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
-    rows = int(rtamd.part_rows(H, rank, world, args.stripe).size)
-    max_rows = max(int(rtamd.part_rows(H, p, world, args.stripe).size) for p in range(world))
-    local_buf = torch.zeros((max_rows, W, 3), dtype=torch.float32, device=dev)
-    frame = torch.zeros((H, W, 3), dtype=torch.float32, device=dev) if rank == 0 else None
-    if world > 1 and rank == 0:
-        gathered = [torch.empty_like(local_buf) for _ in range(world)]
-        src = np.zeros(H, np.int64)
-        for p in range(world):
-            gr = rtamd.part_rows(H, p, world, args.stripe)
-            src[gr] = p * max_rows + np.arange(len(gr))
-        src_index = torch.from_numpy(src).to(dev)
-    else:
-        gathered, src_index = None, None
+    sg = StripeGather(H, W, rank, world, args.stripe, dev)
+    local_buf = sg.local
 
     def step():
         ctx.trace_rows_device(cam, cfg, rank, world, args.stripe, local_buf.data_ptr(), sp)
-        if world > 1:
-            dist.gather(local_buf, gathered if rank == 0 else None, dst=0)
-            if rank == 0:
-                flat = torch.stack(gathered).view(world * max_rows, W, 3)
-                torch.index_select(flat, 0, src_index, out=frame)
-        elif rank == 0:
-            frame.copy_(local_buf[:H])
+        sg.gather()
 
     # work counters of one frame (untimed STATS launch): segments and algorithmic bytes
     _, st = ctx.trace_rows_device(cam, cfg, rank, world, args.stripe, local_buf.data_ptr(), sp, stats=True)
@@ -162,6 +217,15 @@ def main():
                     bytes_formula="48*n_ret+32*n_slot+40*n_loc+32*n_cull+80*n_exact+44*n_hit+36*primary",
                     bytes_reference_equivalent=local_bytes_ref,
                     reference_equivalent_formula="SURVEY 8d: 48*n_ret+32*n_slot+40*n_loc+36*n_sph+36*n_box+76*n_tri+40*n_hit+12*primary")
+
+    traffic = None
+    if rank == 0 and world == 1 and not args.no_traffic:
+        traffic, err = hbm_traffic(args.config, args.stripe)
+        if traffic is not None:
+            roofline["traffic"] = traffic["bytes"]
+            roofline["traffic_detail"] = traffic
+        else:
+            roofline["traffic_note"] = err
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:

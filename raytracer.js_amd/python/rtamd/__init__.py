@@ -194,8 +194,5 @@ class Context:
 
 def part_rows(H, part, n_parts, stripe):
     """Global row indices owned by `part` in stripe order (mirrors rt_part_rows)."""
-    rows = []
-    n_stripes = (H + stripe - 1) // stripe
-    for s in range(part, n_stripes, n_parts):
-        rows.extend(range(s * stripe, min(H, (s + 1) * stripe)))
-    return np.array(rows, dtype=np.int64)
+    from .stripes import part_rows as _pr
+    return _pr(H, part, n_parts, stripe)

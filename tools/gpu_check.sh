@@ -20,6 +20,6 @@ step build 600 python -c "import __graft_entry__ as g; g.build()"
 [ "${SKIP_BENCH:-0}" = 1 ] || step bench 900 python bench.py ${BENCH_ARGS:-}
 if [ "${PROF:-0}" = 1 ]; then
   export TMPDIR=/tmp
-  step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --cpu-budget 0 ${BENCH_ARGS:-}
+  step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --cpu-budget 0 --no-traffic ${BENCH_ARGS:-}
 fi
 echo "== done"

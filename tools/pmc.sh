@@ -3,7 +3,7 @@
 # domains combined with --pmc).  Output: $OUT/pmc/<pass>/..._counter_collection.csv
 set -u
 OUT=${OUT:-gpurun_out}
-ARGS=${PMC_BENCH_ARGS:---steps 2 --warmup 0 --cpu-budget 0}
+ARGS=${PMC_BENCH_ARGS:---steps 2 --warmup 0 --cpu-budget 0 --no-traffic}
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 mkdir -p "$OUT/pmc"
 timeout -k 10 120 rocprofv3 -L > "$OUT/pmc/counters_list.txt" 2>&1 || true
