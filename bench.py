@@ -218,6 +218,20 @@ def main():
                     bytes_reference_equivalent=local_bytes_ref,
                     reference_equivalent_formula="SURVEY 8d: 48*n_ret+32*n_slot+40*n_loc+36*n_sph+36*n_box+76*n_tri+40*n_hit+12*primary")
 
+    # PCIe-inclusive rate of the host-buffer entry point (rt_trace_frame: RGB copied back to a host
+    # Float32Array-sized buffer each frame) — reported beside `value`, never as it
+    host = None
+    if rank == 0 and world == 1:
+        rgb_host = np.zeros(W * H * 3, np.float32)
+        ctx.trace_frame(cam, cfg, rgb=rgb_host, ids=False, stats=False)
+        t0 = time.perf_counter()
+        n_host = 3
+        for _ in range(n_host):
+            ctx.trace_frame(cam, cfg, rgb=rgb_host, ids=False, stats=False)
+        host_ms = (time.perf_counter() - t0) / n_host * 1e3
+        host = dict(entry="rt_trace_frame (host RGB buffer)", ms_per_frame=round(host_ms, 3),
+                    value=round(tot["segments"] / (host_ms * 1e-3) / 1e6, 3), unit="Mrays/s")
+
     traffic = None
     if rank == 0 and world == 1 and not args.no_traffic:
         traffic, err = hbm_traffic(args.config, args.stripe)
@@ -251,6 +265,7 @@ def main():
                        "counters": tot, "scene_build_s": round(build_s, 3)},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "pcie_inclusive": host,
         }
         print(json.dumps(rec), flush=True)
     ctx.close()

@@ -480,7 +480,8 @@ __device__ __forceinline__ RayBox make_raybox(const double o[3], const double d[
     rb.ix = safe_inv(d[0]); rb.iy = safe_inv(d[1]); rb.iz = safe_inv(d[2]);
     rb.ok = isfinite(rb.ox) && isfinite(rb.oy) && isfinite(rb.oz) && fabs(d[0]) < 1e30 && fabs(d[1]) < 1e30 &&
             fabs(d[2]) < 1e30 && !isnan(d[0]) && !isnan(d[1]) && !isnan(d[2]) && fabs(o[0]) < 1e30 &&
-            fabs(o[1]) < 1e30 && fabs(o[2]) < 1e30;
+            fabs(o[1]) < 1e30 && fabs(o[2]) < 1e30 &&
+            fmax(fabs(d[0]), fmax(fabs(d[1]), fabs(d[2]))) >= 1e-10;   // safe_inv's clamp stays negligible
     return rb;
 }
 
