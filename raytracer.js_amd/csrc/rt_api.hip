@@ -66,12 +66,12 @@ struct DevBuf {
 }  // namespace
 
 int rt_build_cull(const rt_scene_desc *s, std::vector<RtPrim> &prim, std::vector<RtBvh> &bvh,
-                  std::vector<int32_t> &node_ent, std::vector<int32_t> &prefix, int leaf);
+                  std::vector<int32_t> &node_ent, std::vector<int32_t> &prefix, bool sah);
 
 struct rt_ctx {
     int device = 0;
     int flags = 0;
-    int bvh_leaf = 1;                // cull-hierarchy leaf size (RT_BVH_LEAF); 1 measured fastest
+    bool bvh_sah = true;             // SAH splits (RT_BVH_SAH=0: median split)
     int occ = 0;
     int diag = 0;
     hipStream_t stream = nullptr;
@@ -107,7 +107,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     c->flags = desc ? desc->flags : 0;
     if (const char *e = getenv("RT_NO_CULL"))
         if (e[0] == '1') c->flags |= RT_CREATE_NO_CULL;
-    if (const char *e = getenv("RT_BVH_LEAF")) c->bvh_leaf = atoi(e);
+    if (const char *e = getenv("RT_BVH_SAH")) c->bvh_sah = atoi(e) != 0;
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     int r = use_device(c);
@@ -238,7 +238,7 @@ extern "C" int rt_upload_scene(rt_ctx *c, const rt_scene_desc *s)
     std::vector<RtBvh> bvh;
     std::vector<int32_t> ent4, prefix;
     if (NL == 0) prim.clear();
-    int r = rt_build_cull(s, prim, bvh, ent4, prefix, c->bvh_leaf);
+    int r = rt_build_cull(s, prim, bvh, ent4, prefix, c->bvh_sah);
     if (r != RT_OK) return r;
     if ((r = use_device(c)) != RT_OK) return r;
     c->has_scene = false;

@@ -2,8 +2,8 @@
 //
 // The reference tests a returned node's entities in EntitySet order and keeps the first one that
 // reports a collision (src/raytracer.ts:186-195).  The GPU reaches the same entity with less work:
-// each node's entity list gets a small binary BVH whose boxes are the entities' AABBs widened by
-// a margin `delta` and rounded outward to f32.  Only entities whose box the ray's half-line
+// each node's entity list gets a small binary BVH (SAH splits, one entity per leaf) whose boxes
+// are the entities' AABBs widened by a margin `delta` and rounded outward to f32.  Only entities whose box the ray's half-line
 // crosses run the exact binary64 test, and the hit with the smallest Set rank wins — the entity
 // the reference's in-order loop stops at.  Entities whose exact test can be ill-conditioned
 // (degenerate triangles, non-finite geometry) get an infinite box and are always tested.
@@ -87,11 +87,59 @@ void prim_bounds(const RtPrim &p, double delta, Item &it)
     for (int i = 0; i < 3; i++) { it.lo[i] -= delta; it.hi[i] += delta; }
 }
 
+// Surface area of a box for the SAH cost, with infinite extents clamped to the scene scale.
+double half_area(const double lo[3], const double hi[3], double clampv)
+{
+    double e[3];
+    for (int i = 0; i < 3; i++) {
+        const double l = std::max(lo[i], -clampv), h = std::min(hi[i], clampv);
+        e[i] = h > l ? h - l : 0.0;
+    }
+    return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
+}
+
 struct Builder {
     std::vector<RtBvh> *bvh;
     std::vector<int> order;     // output slot order (indices into items)
     std::vector<Item> *items;
-    int leaf;
+    bool sah;
+    double clampv;              // SAH area clamp (scene scale)
+    std::vector<double> right_area;
+
+    // Full-sweep SAH over centroid-sorted items on every axis (sets are small: <= a few hundred
+    // entities per node).  Returns the split index; items are left sorted on the chosen axis.
+    int sah_split(int b, int e)
+    {
+        const int n = e - b;
+        double best = INFINITY;
+        int best_axis = -1, best_k = b + n / 2;
+        right_area.resize(n + 1);
+        for (int axis = 0; axis < 3; axis++) {
+            std::sort(items->begin() + b, items->begin() + e, [axis](const Item &x, const Item &y) {
+                return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.slot < y.slot);
+            });
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int k = e - 1; k > b; k--) {
+                const Item &it = (*items)[k];
+                for (int i = 0; i < 3; i++) { lo[i] = std::min(lo[i], it.lo[i]); hi[i] = std::max(hi[i], it.hi[i]); }
+                right_area[k - b] = half_area(lo, hi, clampv);
+            }
+            for (int i = 0; i < 3; i++) { lo[i] = INFINITY; hi[i] = -INFINITY; }
+            for (int k = b + 1; k < e; k++) {
+                const Item &it = (*items)[k - 1];
+                for (int i = 0; i < 3; i++) { lo[i] = std::min(lo[i], it.lo[i]); hi[i] = std::max(hi[i], it.hi[i]); }
+                const double cost = half_area(lo, hi, clampv) * (k - b) + right_area[k - b] * (e - k);
+                if (cost < best) { best = cost; best_axis = axis; best_k = k; }
+            }
+        }
+        if (best_axis != 2 && best_axis >= 0) {
+            const int axis = best_axis;
+            std::sort(items->begin() + b, items->begin() + e, [axis](const Item &x, const Item &y) {
+                return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.slot < y.slot);
+            });
+        }
+        return best_k;
+    }
 
     void emit(int b, int e)     // items [b, e) of *items (already permuted in place)
     {
@@ -108,19 +156,24 @@ struct Builder {
         }
         RtBvh node;
         for (int i = 0; i < 3; i++) { node.lo[i] = round_down(lo[i]); node.hi[i] = round_up(hi[i]); }
-        if (e - b <= leaf) {
-            node.info = ((int)order.size() << 4) | (e - b);
-            for (int k = b; k < e; k++) order.push_back(k);
+        if (e - b == 1) {
+            node.info = ((int)order.size() << 4) | 1;     // leaf: first prim slot << 4 | count
+            order.push_back(b);
         } else {
-            int axis = 0;
-            double ext = -1;
-            for (int i = 0; i < 3; i++)
-                if (chi[i] - clo[i] > ext) { ext = chi[i] - clo[i]; axis = i; }
-            const int mid = b + (e - b) / 2;
-            std::nth_element(items->begin() + b, items->begin() + mid, items->begin() + e,
-                             [axis](const Item &x, const Item &y) {
-                                 return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.slot < y.slot);
-                             });
+            int mid;
+            if (sah) {
+                mid = sah_split(b, e);
+            } else {
+                int axis = 0;
+                double ext = -1;
+                for (int i = 0; i < 3; i++)
+                    if (chi[i] - clo[i] > ext) { ext = chi[i] - clo[i]; axis = i; }
+                mid = b + (e - b) / 2;
+                std::nth_element(items->begin() + b, items->begin() + mid, items->begin() + e,
+                                 [axis](const Item &x, const Item &y) {
+                                     return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.slot < y.slot);
+                                 });
+            }
             node.info = -1;
             (*bvh)[me] = node;
             emit(b, mid);
@@ -136,15 +189,13 @@ struct Builder {
 // prim: all records in global list order (rank = index).  Rewrites `prim` into per-node cull
 // order, fills `bvh`, node_ent (4 ints per node) and the Set-order type prefix counts.
 int rt_build_cull(const rt_scene_desc *s, std::vector<RtPrim> &prim, std::vector<RtBvh> &bvh,
-                  std::vector<int32_t> &node_ent, std::vector<int32_t> &prefix, int leaf)
+                  std::vector<int32_t> &node_ent, std::vector<int32_t> &prefix, bool sah)
 {
     const int N = s->n_nodes;
     double scale = fabs(s->node_size[0]);
     for (int i = 0; i < 3; i++)
         scale = std::max(scale, std::max(fabs(s->node_pos[i]), fabs(s->node_pos[i] + s->node_size[0])));
     const double delta = ldexp(scale, -13);          // ~1.2e-4 x scene scale
-    if (leaf < 1) leaf = 1;
-    if (leaf > 15) leaf = 15;
     node_ent.assign(4 * (size_t)N, 0);
     prefix.assign(4 * (size_t)(s->n_list ? s->n_list : 1), 0);
     bvh.clear();
@@ -167,7 +218,7 @@ int rt_build_cull(const rt_scene_desc *s, std::vector<RtPrim> &prim, std::vector
             items[k].slot = k;
         }
         const int root = (int)bvh.size();
-        Builder B{&bvh, {}, &items, leaf};
+        Builder B{&bvh, {}, &items, sah, 4 * scale, {}};
         B.order.reserve(c);
         B.emit(0, c);
         const int end = (int)bvh.size();
