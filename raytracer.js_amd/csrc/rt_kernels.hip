@@ -119,6 +119,7 @@ struct Walker {
 
 struct Counters {
     long long ret, slot, loc, sph, box, tri, hit, steps, cull, exact;
+    long long cyc_walk, cyc_test, cyc_tile;   // diag bit 3 (stats build): lane-cycle attribution
 };
 
 // setup_cur_node — :251-278.  Returns 1/0 or -1 (throw).
@@ -680,7 +681,9 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
     if (walker_set(S, w, o, d, F.start_tree >= 0, F.start_tree, F.start_oct, c) < 0) { R.status = ST_FAULT; goto done; }
     for (;;) {
         int node, pt, po;
+        const long long tw0 = (STATS && (diag & 8)) ? (long long)clock64() : 0;
         const int r = walker_next<false>(S, w, node, pt, po, c);
+        if (STATS && (diag & 8)) c.cyc_walk += (long long)clock64() - tw0;
         if (r < 0) { R.status = r == -2 ? ST_CAP : ST_FAULT; goto done; }
         if (r == 0) break;
         // for (entity of node.value.set): first collision in Set order wins
@@ -695,7 +698,9 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
             const double lvl = log2(S.node_ps[0 * 4 + 3] / S.node_ps[4 * node + 3]);
             box_ctr = lvl < 1.5 ? &c.cull : (lvl < 3.5 ? &c.exact : &dummy);
         }
+        const long long tt0 = (STATS && (diag & 8)) ? (long long)clock64() : 0;
         const int hk = node_first_hit<STATS>(S, ent, o, d, rb, cull, c, *box_ctr, h, rank);
+        if (STATS && (diag & 8)) c.cyc_test += (long long)clock64() - tt0;
         if (hk < 0) continue;
         const RtPrim &pr = S.prim[hk];
         if (prim_hit(pr, o, d, h) < 0) { R.status = ST_FAULT; goto done; }   // recompute the winner's hit
@@ -775,13 +780,14 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
     const int n_tiles = tiles_x * ((L.rows + 7) >> 3);
     const RtFrameSetup F = *L.setup;
     const size_t plane = (size_t)L.rows * (size_t)W;
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     long long n_seg = 0, n_prim = 0, n_warn = 0, n_fault = 0;
     for (;;) {
         int t = 0;
         if (lane == 0) t = atomicAdd(L.tile_counter, 1);
         t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
         if (t >= n_tiles) break;
+        const long long t_tile = (STATS && (L.diag & 8)) ? (long long)clock64() : 0;
         const int ty = t / tiles_x, tx = t - ty * tiles_x;
         const int x = tx * 8 + (lane & 7);
         const int lr = ty * 8 + (lane >> 3);
@@ -813,9 +819,15 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
             n_prim += 1;
             n_warn += R.status == ST_WARN;
             n_fault += R.status == ST_FAULT || R.status == ST_CAP;
+            if (L.diag & 8) c.cyc_tile += (long long)clock64() - t_tile;
         }
     }
     if (STATS) {
+        if (L.diag & 8) {
+            // diag bit 3: n_loc / n_cull / n_exact report lane-cycles per tile / in walker_next /
+            // in the node entity tests (s_memtime), summed over lanes
+            c.loc = c.cyc_tile; c.cull = c.cyc_walk; c.exact = c.cyc_test;
+        }
         long long v[CT_N] = {n_seg, c.ret, c.slot, c.loc, c.sph, c.box, c.tri, c.hit,
                              n_prim, n_warn, n_fault, c.cull, c.exact};
 #pragma unroll
@@ -831,7 +843,7 @@ __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, doub
                              int max_out, int32_t *out_tree, int32_t *out_oct, int32_t *n_out)
 {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Walker w;
     const double o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz};
     int n = 0;

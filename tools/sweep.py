@@ -51,9 +51,14 @@ def main():
         s.synchronize()
         wall = (time.perf_counter() - t0) / a.frames * 1e3
         kt = ctx.kernel_times(a.frames)
+        extra = {}
+        if int(os.environ.get("RT_DIAG", "0")) & 8:
+            tile = st.n_loc
+            extra = dict(lane_cycles_tile=tile, frac_walk=round(st.n_cull / tile, 3), frac_test=round(st.n_exact / tile, 3),
+                         frac_other=round(1 - (st.n_cull + st.n_exact) / tile, 3))
         rec = dict(variant=name, env=kv, kernel_ms=round(float(kt.mean()), 3), kernel_min=round(float(kt.min()), 3),
                    wall_ms=round(wall, 3), mrays=round(st.segments / (wall * 1e-3) / 1e6, 2),
-                   n_cull=st.n_cull, n_exact=st.n_exact, segments=st.segments)
+                   n_cull=st.n_cull, n_exact=st.n_exact, segments=st.segments, **extra)
         print(json.dumps(rec), flush=True)
         ctx.close()
 
