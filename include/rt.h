@@ -156,6 +156,9 @@ typedef struct rt_create_desc {
 /* Disable the per-node cull hierarchies: every entity of a returned node runs the exact test
  * (verification mode; results are identical by construction). */
 #define RT_CREATE_NO_CULL 1
+/* Run each frame as one fused trace kernel instead of the walk pass + test pass (verification
+ * mode; results are identical by construction). */
+#define RT_CREATE_NO_SPLIT 2
 
 int  rt_create(const rt_create_desc *desc, rt_ctx **out);
 void rt_destroy(rt_ctx *ctx);

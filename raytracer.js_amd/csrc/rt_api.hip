@@ -72,6 +72,8 @@ struct rt_ctx {
     int device = 0;
     int flags = 0;
     bool bvh_sah = true;             // SAH splits (RT_BVH_SAH=0: median split)
+    bool split = true;               // walk pass + test pass (RT_SPLIT=0: fused k_trace)
+    int cand_cap = 64;               // candidate nodes per pixel in the split path (RT_CAND_CAP)
     int occ = 0;
     int diag = 0;
     hipStream_t stream = nullptr;
@@ -80,7 +82,7 @@ struct rt_ctx {
     RtDevScene scene{};
     DevBuf b_node_ps, b_node_child, b_node_up, b_node_ent, b_prim, b_shades, b_ent_sub, b_sub_ri;
     DevBuf b_bvh, b_list, b_prefix;
-    DevBuf b_setup, b_fr, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
+    DevBuf b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_fr, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
     DevBuf b_walk;
     static constexpr int NEV = 256;
     hipEvent_t ev[NEV][2] = {};
@@ -108,6 +110,9 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_NO_CULL"))
         if (e[0] == '1') c->flags |= RT_CREATE_NO_CULL;
     if (const char *e = getenv("RT_BVH_SAH")) c->bvh_sah = atoi(e) != 0;
+    if (const char *e = getenv("RT_SPLIT")) c->split = atoi(e) != 0;
+    if (c->flags & RT_CREATE_NO_SPLIT) c->split = false;
+    if (const char *e = getenv("RT_CAND_CAP")) c->cand_cap = atoi(e) < 1 ? 1 : atoi(e);
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     int r = use_device(c);
@@ -118,7 +123,8 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
             r = rt_set_error(RT_E_HIP, "rt_create: hipEventCreate failed");
     if (r == RT_OK) r = c->b_setup.ensure(sizeof(RtFrameSetup));
     if (r == RT_OK) r = c->b_counters.ensure(sizeof(unsigned long long) * CT_N);
-    if (r == RT_OK) r = c->b_fault.ensure(4 * sizeof(int));   // [0] fault flag, [1] tile queue head
+    if (r == RT_OK) r = c->b_fault.ensure(sizeof(int));   // ray fault flag
+    if (r == RT_OK) r = c->b_ctr.ensure(sizeof(int32_t) * RT_CTR_INTS);
     if (r != RT_OK) {
         rt_destroy(c);
         return r;
@@ -133,7 +139,7 @@ extern "C" void rt_destroy(rt_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->b_node_ps, &c->b_node_child, &c->b_node_up, &c->b_node_ent, &c->b_prim,
-                      &c->b_shades, &c->b_ent_sub, &c->b_sub_ri, &c->b_setup, &c->b_fr, &c->b_dirs,
+                      &c->b_shades, &c->b_ent_sub, &c->b_sub_ri, &c->b_cand, &c->b_cand_n, &c->b_first, &c->b_queue, &c->b_ctr, &c->b_setup, &c->b_fr, &c->b_dirs,
                       &c->b_rgb, &c->b_hit_e, &c->b_hit_n, &c->b_status, &c->b_counters, &c->b_fault,
                       &c->b_walk, &c->b_bvh, &c->b_list, &c->b_prefix};
     for (DevBuf *b : bufs) b->release();
@@ -318,9 +324,29 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.status = want_ids ? (uint8_t *)c->b_status.p : nullptr;
     L.fault = (int32_t *)c->b_fault.p;
     L.cull = (c->flags & RT_CREATE_NO_CULL) ? 0 : 1;
-    L.tile_counter = (int32_t *)c->b_fault.p + 1;
+    L.ctr = (int32_t *)c->b_ctr.p;
     L.occ = c->occ;
     L.diag = c->diag;
+    if (c->split && P > 0) {
+        // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
+        // be allocated the frame runs the fused kernel instead (same results).
+        L.cand_cap = c->cand_cap;
+        if (c->b_cand.ensure(sizeof(int32_t) * (size_t)L.cand_cap * P) == RT_OK &&
+            c->b_cand_n.ensure(sizeof(int32_t) * P) == RT_OK && c->b_first.ensure(2 * sizeof(int32_t) * P) == RT_OK &&
+            c->b_queue.ensure(3 * sizeof(RtCont) * P) == RT_OK) {
+            L.cand = (int32_t *)c->b_cand.p;
+            L.cand_n = (int32_t *)c->b_cand_n.p;
+            L.first = (int32_t *)c->b_first.p;
+            L.queue[0] = (RtCont *)c->b_queue.p;
+            L.queue[1] = L.queue[0] + P;
+            L.ovf = L.queue[1] + P;
+        } else {
+            (void)hipGetLastError();
+            L.cand = nullptr;
+            L.cand_n = nullptr;
+            L.first = nullptr;
+        }
+    }
     return RT_OK;
 }
 

@@ -53,6 +53,15 @@ struct RtDevScene {
     int32_t n_nodes, n_list, n_entities, n_shades, n_subs, n_bvh;
 };
 
+// A ray of the split path at its first continuation (segment start after a mirror / transmission
+// hit), queued by the shading pass for the continuation pass.
+struct alignas(16) RtCont {
+    double o[3], d[3], col[3], path;
+    int32_t refcount, cur_sub, hit_ent, hit_node, segments, pix;
+    int32_t pad[2];
+};
+static_assert(sizeof(RtCont) == 112, "RtCont must stay 112 bytes");
+
 // Per-frame state computed on the device by the setup kernel.
 struct RtFrameSetup {
     int32_t start_tree;   // node_at_pos(otree, camera.pos) → tree (-1: null)
@@ -79,13 +88,23 @@ struct RtLaunch {
     uint8_t *status;                            // device [rows*W] or null
     unsigned long long *counters;               // device [CT_N] or null (stats build)
     int32_t *fault;                             // device flag: some ray hit a reference throw
-    int32_t *tile_counter;                      // device work queue head (zeroed per launch)
     int32_t blend;                              // col_weight != 1: read-modify-write rgb
     int32_t skip_trace;                         // ray generation only (rt_debug_camera_dirs)
     int32_t cull;                               // use the per-node cull hierarchies
     int32_t occ;                                // k_trace occupancy variant (RT_OCC; 0 = default)
     int32_t diag;                               // RT_DIAG bits (timing experiments only; wrong images)
+    int32_t *ctr;                               // device work counters [RT_CTR_INTS] (rt_kernels.hip)
+    // split path; cand == null: fused kernel
+    int32_t *cand;                              // device [cand_cap][rows*W] candidate nodes per ray
+    int32_t *cand_n;                            // device [rows*W] candidate count / walk end status
+    int32_t cand_cap;
+    int32_t *first;                             // device [rows*W] int2 {node, slot}: k_first's result
+    struct RtCont *queue[2];                    // device [rows*W] each: continuations, by level parity
+    struct RtCont *ovf;                         // device [rows*W]: rays left to the fused kernel
+    int32_t level, last_level;                  // set per launch by rt_launch_frame
 };
+
+enum { RT_MAX_LEVELS = 32, RT_CTR_INTS = 4 + 4 * (RT_MAX_LEVELS + 1) };
 
 int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end);
 int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[3], int include_undefined,

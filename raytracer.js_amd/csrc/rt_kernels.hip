@@ -21,6 +21,7 @@ using namespace rtjs;
 namespace {
 
 constexpr int ST_OK = 0, ST_WARN = 1, ST_FAULT = 2, ST_CAP = 3;
+constexpr int ST_DEFER = 100;                    // split path: continuation queued, pixel written later
 constexpr long long STEP_CAP = 1ll << 24;        // per-ray loop bound: every lane terminates
 
 // ---- node access --------------------------------------------------------------------------------
@@ -665,42 +666,129 @@ struct RayResult {
     int hit_ent, hit_node, segments, status;
 };
 
-template <bool STATS>
-__device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg, bool cull,
-                          int diag, const double cam_pos[3], const double dir0[3], RayResult &R, Counters &c)
+// First-segment result of the split path (k_first): the first walker stop with an exact hit and
+// its winning entity.
+struct ListHit {
+    int node, slot, rank;      // slot < 0: no candidate node has a hit
+};
+
+// Continuation queues of the split path.
+struct RayQueues {
+    RtCont *next;              // next bounce level
+    int32_t *next_n;
+    RtCont *ovf;               // rays the fused kernel finishes (k_cont)
+    int32_t *ovf_n;
+    bool last;                 // no next level: continuations go to ovf
+};
+
+__device__ __forceinline__ void queue_push(RtCont *q, int32_t *qn, const double o[3], const double d[3], double col0,
+                                           double col1, double col2, double path, int refcount, int cur_sub,
+                                           const RayResult &R, int pix, int fresh)
 {
-    double o[3] = {cam_pos[0], cam_pos[1], cam_pos[2]};
-    double d[3] = {dir0[0], dir0[1], dir0[2]};
-    double col0 = 1, col1 = 1, col2 = 1;
-    int refcount = 0, cur_sub = F.start_sub;
+    const int k = atomicAdd(qn, 1);
+    RtCont &e = q[k];
+    for (int i = 0; i < 3; i++) { e.o[i] = o[i]; e.d[i] = d[i]; }
+    e.col[0] = col0; e.col[1] = col1; e.col[2] = col2;
+    e.path = path;
+    e.refcount = refcount; e.cur_sub = cur_sub;
+    e.hit_ent = R.hit_ent; e.hit_node = R.hit_node; e.segments = R.segments;
+    e.pix = pix;
+    e.pad[0] = fresh;
+    e.pad[1] = 0;
+}
+
+// Trace modes, all running the same bounce loop (src/raytracer.ts:168-277):
+//   TR_FUSED   walks every segment (state from the camera, or from record `rs`);
+//   TR_LIST    the first segment (primary ray, or the queued segment `rs`) was resolved by k_walk +
+//              k_first: `pre` is its first walker stop with a hit, or none and the walk's end
+//              (cn & 3: 0 finished, 1 throw, 2 step cap, 3 the segment's set_pos_and_dir threw).
+//              A continuation is queued for the next level (status ST_DEFER); this mode never walks.
+// A record with pad[0] != 0 is a fresh primary ray; otherwise it sits at a segment start (the
+// walker re-seat of src/raytracer.ts:254 is still to do).
+enum { TR_FUSED = 0, TR_LIST = 1 };
+
+template <bool STATS, int MODE>
+__device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg, bool cull,
+                          int diag, const double cam_pos[3], const double dir0[3], RayResult &R, Counters &c,
+                          int cn, const ListHit &pre, const RtCont *rs, const RayQueues &Q, int pix)
+{
+    constexpr bool LIST = MODE == TR_LIST;
+    double o[3], d[3];
+    double col0, col1, col2, path;
+    int refcount, cur_sub;
     bool light_hit = false;
-    double path = 0;
-    RayBox rb = make_raybox(o, d);
-    R.hit_ent = -1; R.hit_node = -1; R.segments = 1; R.status = ST_OK;
+    RayBox rb;
     Walker w;
-    if (walker_set(S, w, o, d, F.start_tree >= 0, F.start_tree, F.start_oct, c) < 0) { R.status = ST_FAULT; goto done; }
+    bool seat = false;           // segment start: re-seat the walker at (o, d) (src/raytracer.ts:254)
+    bool first_stop = true;      // TR_LIST: the resolved stop not yet consumed
+    R.status = ST_OK;
+    if (rs) {
+        for (int i = 0; i < 3; i++) { o[i] = rs->o[i]; d[i] = rs->d[i]; }
+        col0 = rs->col[0]; col1 = rs->col[1]; col2 = rs->col[2];
+        path = rs->path;
+        refcount = rs->refcount;
+        cur_sub = rs->cur_sub;
+        R.hit_ent = rs->hit_ent; R.hit_node = rs->hit_node; R.segments = rs->segments;
+        seat = !rs->pad[0];
+    } else {
+        for (int i = 0; i < 3; i++) { o[i] = cam_pos[i]; d[i] = dir0[i]; }
+        col0 = col1 = col2 = 1;
+        path = 0;
+        refcount = 0;
+        cur_sub = F.start_sub;
+        R.hit_ent = -1; R.hit_node = -1; R.segments = 1;
+    }
+    if (!seat) {
+        rb = make_raybox(o, d);
+        if (!LIST && walker_set(S, w, o, d, F.start_tree >= 0, F.start_tree, F.start_oct, c) < 0) {
+            R.status = ST_FAULT;
+            goto done;
+        }
+    }
     for (;;) {
-        int node, pt, po;
+        if (seat) {
+            seat = false;
+            if (LIST) {
+                if ((cn & 3) == 3) { R.status = ST_FAULT; goto done; }                   // k_walk's seat threw
+            } else {
+                if (walker_set(S, w, o, d, false, 0, 0, c) < 0) { R.status = ST_FAULT; goto done; }   // :254
+            }
+            if (refcount >= cfg.refmax) { col0 = col1 = col2 = 0; goto done; }                 // COLOR_BLACK
+            R.segments++;
+            rb = make_raybox(o, d);
+        }
+        int node, pt, po, r;
         const long long tw0 = (STATS && (diag & 8)) ? (long long)clock64() : 0;
-        const int r = walker_next<false>(S, w, node, pt, po, c);
+        if (LIST) {
+            if (first_stop && pre.slot >= 0) { node = pre.node; r = 1; }
+            else r = (cn & 3) == 0 ? 0 : ((cn & 3) == 2 ? -2 : -1);
+            first_stop = false;
+        } else {
+            r = walker_next<false>(S, w, node, pt, po, c);
+        }
         if (STATS && (diag & 8)) c.cyc_walk += (long long)clock64() - tw0;
         if (r < 0) { R.status = r == -2 ? ST_CAP : ST_FAULT; goto done; }
         if (r == 0) break;
-        // for (entity of node.value.set): first collision in Set order wins
-        const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
-        if (ent.y == 0 || (diag & 1)) continue;        // diag bit 0: walker-only timing
         Hit h;
-        int rank;
-        long long *box_ctr = &c.cull;
-        long long dummy = 0;
-        if (STATS && (diag & 2)) {
-            // diag bit 1 (stats only): n_cull counts box tests of octree levels 0-1, n_exact of 2-3
-            const double lvl = log2(S.node_ps[0 * 4 + 3] / S.node_ps[4 * node + 3]);
-            box_ctr = lvl < 1.5 ? &c.cull : (lvl < 3.5 ? &c.exact : &dummy);
+        int rank, hk;
+        if (LIST) {
+            hk = pre.slot;
+            rank = pre.rank;
+        } else {
+            // for (entity of node.value.set): first collision in Set order wins
+            const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
+            if (ent.y == 0 || (diag & 1)) continue;        // diag bit 0: walker-only timing
+            long long *box_ctr = &c.cull;
+            long long dummy = 0;
+            if (STATS && (diag & 2)) {
+                // diag bit 1 (stats only): n_cull counts box tests of octree levels 0-1, n_exact of 2-3
+                const double lvl = log2(S.node_ps[0 * 4 + 3] / S.node_ps[4 * node + 3]);
+                box_ctr = lvl < 1.5 ? &c.cull : (lvl < 3.5 ? &c.exact : &dummy);
+            }
+            const long long tt0 = (STATS && (diag & 8)) ? (long long)clock64() : 0;
+            hk = node_first_hit<STATS>(S, ent, o, d, rb, cull, c, *box_ctr, h, rank);
+            if (STATS && (diag & 8)) c.cyc_test += (long long)clock64() - tt0;
         }
-        const long long tt0 = (STATS && (diag & 8)) ? (long long)clock64() : 0;
-        const int hk = node_first_hit<STATS>(S, ent, o, d, rb, cull, c, *box_ctr, h, rank);
-        if (STATS && (diag & 8)) c.cyc_test += (long long)clock64() - tt0;
         if (hk < 0) continue;
         const RtPrim &pr = S.prim[hk];
         if (prim_hit(pr, o, d, h) < 0) { R.status = ST_FAULT; goto done; }   // recompute the winner's hit
@@ -750,10 +838,19 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         } else {
             goto done;
         }
-        if (walker_set(S, w, o, d, false, 0, 0, c) < 0) { R.status = ST_FAULT; goto done; }   // :254
-        if (refcount >= cfg.refmax) { col0 = col1 = col2 = 0; goto done; }                 // COLOR_BLACK
-        R.segments++;
-        rb = make_raybox(o, d);
+        if (LIST) {
+            if (refcount >= cfg.refmax) {
+                // the next segment start ends the ray: set_pos_and_dir (may throw), then COLOR_BLACK
+                if (walker_set(S, w, o, d, false, 0, 0, c) < 0) { R.status = ST_FAULT; goto done; }
+                col0 = col1 = col2 = 0;
+                goto done;
+            }
+            queue_push(Q.last ? Q.ovf : Q.next, Q.last ? Q.ovf_n : Q.next_n, o, d, col0, col1, col2, path, refcount,
+                       cur_sub, R, pix, 0);
+            R.status = ST_DEFER;
+            return;
+        }
+        seat = true;
     }
     if (!light_hit) {
         col0 = col0 * cfg.sky_rgb[0]; col1 = col1 * cfg.sky_rgb[1]; col2 = col2 * cfg.sky_rgb[2];
@@ -766,54 +863,111 @@ done:
     R.rgb[0] = col0; R.rgb[1] = col1; R.rgb[2] = col2;
 }
 
+// ExposureBuffer.set_color_i: c*w + old*(1-w), stored as f32 (src/view/exposure_buffer.ts:77-91),
+// plus the parity outputs.
+__device__ __forceinline__ void write_pixel(const RtLaunch &L, size_t pix, const RayResult &R)
+{
+    const double wgt = L.cfg.col_weight;
+    float *px = L.rgb + 3 * pix;
+    for (int k = 0; k < 3; k++) {
+        const double old = L.blend ? (double)px[k] : 0.0;
+        double v = R.rgb[k] * wgt;
+        v += old * (1 - wgt);
+        px[k] = (float)v;
+    }
+    if (L.hit_entity) L.hit_entity[pix] = R.hit_ent;
+    if (L.hit_node) L.hit_node[pix] = R.hit_node;
+    if (L.status) L.status[pix] = (uint8_t)R.status;
+    if (R.status >= ST_FAULT && L.fault) atomicOr(L.fault, 1);
+}
+
+// ---- work distribution ------------------------------------------------------------------------------------
+// Device counters (L.ctr): [0] overflow queue count, [1] its read head; per level lv (0 = primary
+// rays, >= 1 = continuation levels) a block at 4 + 4*lv: {count of the queue written at this
+// level, work head of k_walk, of k_first, of k_shade}.  Level lv reads queue (lv-1)&1 and writes
+// queue lv&1.
+__device__ __forceinline__ int32_t *lvl_ctr(const RtLaunch &L, int lv) { return L.ctr + 4 + 4 * lv; }
+
+__device__ __forceinline__ int claim(int32_t *head, int lane)
+{
+    int t = 0;
+    if (lane == 0) t = atomicAdd(head, 1);
+    return __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+}
+
+// A lane's ray of one work item: level 0 items are 8x8 pixel tiles (one lane per pixel), higher
+// levels take 64 queue records per item.  `id` indexes the per-ray pass buffers.
+struct RaySrc {
+    bool valid;
+    size_t id;
+    int pix;
+    const RtCont *rec;         // null for primary rays
+    double o[3], d[3];
+};
+
+__device__ __forceinline__ int n_items(const RtLaunch &L)
+{
+    if (L.level == 0) return ((L.cam.width + 7) >> 3) * ((L.rows + 7) >> 3);
+    return (*lvl_ctr(L, L.level - 1) + 63) >> 6;
+}
+
+__device__ __forceinline__ void ray_src(const RtLaunch &L, int item, int lane, RaySrc &r)
+{
+    if (L.level == 0) {
+        const int W = L.cam.width;
+        const int tiles_x = (W + 7) >> 3;
+        const int ty = item / tiles_x, tx = item - ty * tiles_x;
+        const int x = tx * 8 + (lane & 7), lr = ty * 8 + (lane >> 3);
+        r.valid = x < W && lr < L.rows;
+        r.rec = nullptr;
+        if (!r.valid) return;
+        r.id = (size_t)lr * (size_t)W + (size_t)x;
+        r.pix = (int)r.id;
+        const size_t plane = (size_t)L.rows * (size_t)W;
+        const size_t di = (size_t)x * (size_t)L.rows + (size_t)lr;           // x-major (k_raygen)
+        for (int i = 0; i < 3; i++) { r.o[i] = L.cam.pos[i]; r.d[i] = L.dirs[(size_t)i * plane + di]; }
+    } else {
+        const int q = item * 64 + lane;
+        r.valid = q < *lvl_ctr(L, L.level - 1);
+        if (!r.valid) return;
+        r.id = (size_t)q;
+        r.rec = L.queue[(L.level - 1) & 1] + q;
+        r.pix = r.rec->pix;
+        for (int i = 0; i < 3; i++) { r.o[i] = r.rec->o[i]; r.d[i] = r.rec->d[i]; }
+    }
+}
+
 // One lane per pixel of this part; 256-lane blocks cover 16x16 pixel tiles, each wave an 8x8 tile.
 // Persistent waves: each wave repeatedly takes the next 8x8 pixel tile from an atomic queue
 // (one returning atomic per tile, lane 0) and traces it one ray per lane.  Per-ray cost varies by
 // orders of magnitude across the frame (rays that hit early vs rays that cross every upper-level
 // set), so wave-granular dynamic scheduling replaces the fixed block->tile mapping and its tail.
+// The fused kernel: the stats build, and the RT_CREATE_NO_SPLIT path.
 template <bool STATS, int MINW>
 __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
 {
-    const int W = L.cam.width;
     const int lane = threadIdx.x & 63;
-    const int tiles_x = (W + 7) >> 3;
-    const int n_tiles = tiles_x * ((L.rows + 7) >> 3);
+    const int n_tiles = n_items(L);
     const RtFrameSetup F = *L.setup;
-    const size_t plane = (size_t)L.rows * (size_t)W;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     long long n_seg = 0, n_prim = 0, n_warn = 0, n_fault = 0;
+    const ListHit none = {-1, -1, 0};
+    const RayQueues Q = {nullptr, nullptr, nullptr, nullptr, false};
     for (;;) {
-        int t = 0;
-        if (lane == 0) t = atomicAdd(L.tile_counter, 1);
-        t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+        const int t = claim(lvl_ctr(L, 0) + 1, lane);
         if (t >= n_tiles) break;
         const long long t_tile = (STATS && (L.diag & 8)) ? (long long)clock64() : 0;
-        const int ty = t / tiles_x, tx = t - ty * tiles_x;
-        const int x = tx * 8 + (lane & 7);
-        const int lr = ty * 8 + (lane >> 3);
-        if (x >= W || lr >= L.rows) continue;
+        RaySrc src;
+        ray_src(L, t, lane, src);
+        if (!src.valid) continue;
         RayResult R;
-        const size_t pix = (size_t)lr * (size_t)W + (size_t)x;
-        const size_t di = (size_t)x * (size_t)L.rows + (size_t)lr;           // x-major (k_raygen)
-        const double dir0[3] = {L.dirs[di], L.dirs[plane + di], L.dirs[2 * plane + di]};
         if (F.fault) {
             R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.segments = 1; R.status = ST_FAULT;
         } else {
-            trace_ray<STATS>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, dir0, R, c);
+            trace_ray<STATS, TR_FUSED>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, -1, none,
+                                       nullptr, Q, src.pix);
         }
-        // ExposureBuffer.set_color_i: c*w + old*(1-w), stored as f32 (src/view/exposure_buffer.ts:77-91)
-        const double wgt = L.cfg.col_weight;
-        float *px = L.rgb + 3 * pix;
-        for (int k = 0; k < 3; k++) {
-            const double old = L.blend ? (double)px[k] : 0.0;
-            double v = R.rgb[k] * wgt;
-            v += old * (1 - wgt);
-            px[k] = (float)v;
-        }
-        if (L.hit_entity) L.hit_entity[pix] = R.hit_ent;
-        if (L.hit_node) L.hit_node[pix] = R.hit_node;
-        if (L.status) L.status[pix] = (uint8_t)R.status;
-        if (R.status >= ST_FAULT && L.fault) atomicOr(L.fault, 1);
+        write_pixel(L, src.id, R);
         if (STATS) {
             n_seg += R.segments;
             n_prim += 1;
@@ -835,6 +989,158 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
             const long long s = wave_sum(v[k]);
             if (lane == 0 && s) atomicAdd(L.counters + k, (unsigned long long)s);
         }
+    }
+}
+
+// ---- the split path ------------------------------------------------------------------------
+// Pass 1: each ray's OctreeWalker stops, filtered to nodes with entities whose cull-root box the ray
+// crosses (no entity of any other node can be hit), appended in order to a per-ray list [k][id];
+// cand_n = count * 4 + end (0 walk finished, 1 throw, 2 step cap, 3 the continuation's
+// set_pos_and_dir threw), or -1 when the list overflowed.  The walker alone needs ~120 VGPRs
+// (4 waves/SIMD) against the fused kernel's 168 (3 waves).
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
+{
+    const int lane = threadIdx.x & 63;
+    const int items = n_items(L);
+    const RtFrameSetup F = *L.setup;
+    const RtDevScene &S = L.scene;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (;;) {
+        const int t = claim(lvl_ctr(L, L.level) + 1, lane);
+        if (t >= items) break;
+        RaySrc src;
+        ray_src(L, t, lane, src);
+        if (!src.valid) continue;
+        const RayBox rb = make_raybox(src.o, src.d);
+        Walker w;
+        int n = 0, end = 0;
+        const bool seated = src.rec ? walker_set(S, w, src.o, src.d, false, 0, 0, c) >= 0
+                                    : !F.fault && walker_set(S, w, src.o, src.d, F.start_tree >= 0, F.start_tree,
+                                                             F.start_oct, c) >= 0;
+        if (!seated) {
+            end = src.rec ? 3 : 1;
+        } else {
+            for (;;) {
+                int node, pt, po;
+                const int r = walker_next<false>(S, w, node, pt, po, c);
+                if (r < 0) { end = r == -2 ? 2 : 1; break; }
+                if (r == 0) break;
+                const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
+                if (ent.y == 0) continue;
+                if (L.cull && rb.ok && !ray_box(S.bvh[ent.z], rb)) continue;
+                if (n < L.cand_cap) L.cand[(size_t)n * stride + src.id] = node;
+                n++;
+            }
+        }
+        L.cand_n[src.id] = n > L.cand_cap ? -1 : n * 4 + end;
+    }
+}
+
+// Pass 2: for each ray, the first candidate node (walk order) with an exact hit and its winning prim
+// slot (node_first_hit: minimum Set rank), written as first[id] = {node, slot} or {-1, -1}.  Only
+// the candidate scan lives here: its cull traversal is a chain of dependent loads, and a lane
+// pays the sum of its own node tests rather than, as in the fused kernel, the maximum over the
+// wave at every walker stop.
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
+{
+    const int lane = threadIdx.x & 63;
+    const int items = n_items(L);
+    const RtDevScene &S = L.scene;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    const bool fault = L.setup->fault != 0;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (;;) {
+        const int t = claim(lvl_ctr(L, L.level) + 2, lane);
+        if (t >= items) break;
+        RaySrc src;
+        ray_src(L, t, lane, src);
+        if (!src.valid) continue;
+        const int cn = L.cand_n[src.id];
+        int2 res = make_int2(-1, -1);
+        if (cn >= 4 && !fault) {
+            const RayBox rb = make_raybox(src.o, src.d);
+            const int n = cn >> 2;
+            for (int k = 0; k < n; k++) {
+                const int node = L.cand[(size_t)k * stride + src.id];
+                const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
+                Hit h;
+                int rank;
+                long long box = 0;
+                const int hk = node_first_hit<false>(S, ent, src.o, src.d, rb, L.cull != 0, c, box, h, rank);
+                if (hk >= 0) { res = make_int2(node, hk); break; }
+            }
+        }
+        reinterpret_cast<int2 *>(L.first)[src.id] = res;
+    }
+}
+
+// Pass 3: shading of the resolved segment; pixels whose ray ends are written, continuations are
+// queued for the next level, overflowed lists go to the fused kernel (k_cont).
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
+{
+    const int lane = threadIdx.x & 63;
+    const int items = n_items(L);
+    const RtFrameSetup F = *L.setup;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const RayQueues Q = {L.queue[L.level & 1], lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
+    for (;;) {
+        const int t = claim(lvl_ctr(L, L.level) + 3, lane);
+        if (t >= items) break;
+        RaySrc src;
+        ray_src(L, t, lane, src);
+        if (!src.valid) continue;
+        RayResult R;
+        if (F.fault) {
+            R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.segments = 1; R.status = ST_FAULT;
+            write_pixel(L, (size_t)src.pix, R);
+            continue;
+        }
+        const int cn = L.cand_n[src.id];
+        if (cn < 0) {
+            // the candidate list overflowed: the fused kernel traces this ray (from its segment start)
+            if (src.rec) {
+                const int k = atomicAdd(L.ctr, 1);
+                L.ovf[k] = *src.rec;
+            } else {
+                R.hit_ent = -1; R.hit_node = -1; R.segments = 1;
+                queue_push(L.ovf, L.ctr, src.o, src.d, 1, 1, 1, 0, 0, F.start_sub, R, src.pix, 1);
+            }
+            continue;
+        }
+        const int2 fh = reinterpret_cast<const int2 *>(L.first)[src.id];
+        const ListHit pre = {fh.x, fh.y, fh.y >= 0 ? L.scene.prim[fh.y].rank : 0};
+        trace_ray<false, TR_LIST>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, cn, pre, src.rec, Q,
+                                  src.pix);
+        if (R.status == ST_DEFER) continue;
+        write_pixel(L, (size_t)src.pix, R);
+    }
+}
+
+// Pass 4: rays the split passes could not finish (overflowed candidate lists, or bounce levels
+// beyond the last launched one), traced by the fused loop from their record.
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
+{
+    const int lane = threadIdx.x & 63;
+    const int n = L.ctr[0];
+    const RtFrameSetup F = *L.setup;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const ListHit none = {-1, -1, 0};
+    const RayQueues Q = {nullptr, nullptr, nullptr, nullptr, false};
+    for (;;) {
+        const int base = claim(L.ctr + 1, lane) * 64;
+        if (base >= n) break;
+        const int q = base + lane;
+        if (q >= n) continue;
+        const RtCont *e = L.ovf + q;
+        RayResult R;
+        trace_ray<false, TR_FUSED>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, e->d, R, c, -1, none, e, Q,
+                                   e->pix);
+        write_pixel(L, (size_t)e->pix, R);
     }
 }
 
@@ -900,14 +1206,34 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     HIP_TRY(hipGetLastError());
     if (L.skip_trace) return RT_OK;
     (void)W;
-    HIP_TRY(hipMemsetAsync(L.tile_counter, 0, sizeof(int32_t), st));
+    HIP_TRY(hipMemsetAsync(L.ctr, 0, sizeof(int32_t) * RT_CTR_INTS, st));
     if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
     // occupancy variants (waves per SIMD the register allocation must admit); RT_OCC selects
-    if (L.counters) launch_persistent(k_trace<true, 2>, st, L);
-    else if (L.occ == 2) launch_persistent(k_trace<false, 2>, st, L);
-    else if (L.occ == 4) launch_persistent(k_trace<false, 4>, st, L);
-    else if (L.occ == 5) launch_persistent(k_trace<false, 5>, st, L);
-    else launch_persistent(k_trace<false, 3>, st, L);
+    if (L.counters) {
+        launch_persistent(k_trace<true, 2>, st, L);
+    } else if (!L.cand) {
+        if (L.occ == 2) launch_persistent(k_trace<false, 2>, st, L);
+        else if (L.occ == 4) launch_persistent(k_trace<false, 4>, st, L);
+        else launch_persistent(k_trace<false, 3>, st, L);
+    } else {
+        // split path: per bounce level a walk pass, a first-hit pass and a shading pass; level 0
+        // takes the primary rays by tiles, level lv >= 1 the continuations queued at lv - 1.  Rays
+        // reaching refmax end inside the shading pass, so refmax - 1 levels carry all bounces.
+        const long long want = (long long)L.cfg.refmax - 1;
+        const int levels = (int)(want < 0 ? 0 : (want > RT_MAX_LEVELS ? RT_MAX_LEVELS : want));
+        for (int lv = 0; lv <= levels; lv++) {
+            RtLaunch Lv = L;
+            Lv.level = lv;
+            Lv.last_level = lv == levels && levels < want;
+            launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lv);
+            HIP_TRY(hipGetLastError());
+            launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv);
+            HIP_TRY(hipGetLastError());
+            launch_persistent(k_shade<3>, st, Lv);
+            HIP_TRY(hipGetLastError());
+        }
+        launch_persistent(k_cont<3>, st, L);
+    }
     HIP_TRY(hipGetLastError());
     if (ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
     return RT_OK;

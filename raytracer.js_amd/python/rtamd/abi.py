@@ -21,6 +21,7 @@ RT_RESP_REFLECTION, RT_RESP_TRANSMISSION, RT_RESP_BOTH = 0, 1, 2
 
 STATUS_OK, STATUS_WARN, STATUS_FAULT, STATUS_CAP = 0, 1, 2, 3
 RT_CREATE_NO_CULL = 1
+RT_CREATE_NO_SPLIT = 2
 
 _d = C.c_double
 _i = C.c_int32

@@ -41,11 +41,25 @@ def _compare(ref, got, pixels=None, exact_rgb=True):
             (rr.view(np.uint32) != gg.view(np.uint32)).any(1).sum())
 
 
+IMAGE_KEYS = ("rgb", "hit_entity", "hit_node", "status")
+
+
+def _same_frames(a, b):
+    for k in IMAGE_KEYS:
+        assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+
+
 def _run_both(ctx, spec, cam, cfg, pixels=None, nthreads=8):
+    """Oracle frame, and the GPU frame from the production kernels (no stats: the split walk/test
+    path); the stats instantiation must produce the identical frame, and its counters are attached."""
     w, root = oracle.build_scene(spec)
     ref = w.trace_frame(root, cam, cfg, pixels=pixels, nthreads=nthreads)
     ctx.upload(rtamd.build_scene(spec))
-    got = ctx.trace_frame(cam, cfg, allow_fault=True)
+    got = ctx.trace_frame(cam, cfg, stats=False, allow_fault=True)
+    st = ctx.trace_frame(cam, cfg, allow_fault=True)
+    _same_frames(got, st)
+    assert got["rc"] == st["rc"]
+    got["stats"] = st["stats"]
     return ref, got
 
 
@@ -193,8 +207,9 @@ def test_exposure_blend(ctx):
     w, root = oracle.build_scene(spec)
     ref = w.trace_frame(root, cam, cfg, rgb=old.copy())
     ctx.upload(rtamd.build_scene(spec))
-    got = ctx.trace_frame(cam, cfg, rgb=old.copy())
+    got = ctx.trace_frame(cam, cfg, rgb=old.copy(), stats=False)
     _compare(ref, got)
+    _same_frames(got, ctx.trace_frame(cam, cfg, rgb=old.copy()))
 
 
 def test_transmission_scene(ctx):
@@ -230,10 +245,38 @@ def test_cull_equals_exhaustive(ctx, name):
         b = ex.trace_frame(cam, cfg, allow_fault=True)
     finally:
         ex.close()
-    for k in ("rgb", "hit_entity", "hit_node", "status"):
-        assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+    _same_frames(a, b)
     assert a["stats"].counters() == b["stats"].counters()
     assert a["stats"].n_exact <= b["stats"].n_exact
+    _same_frames(a, ctx.trace_frame(cam, cfg, stats=False, allow_fault=True))
+
+
+@pytest.mark.parametrize("name", ["config1", "small3", "small8", "config2"])
+def test_split_equals_fused(ctx, name, monkeypatch):
+    """The walk pass + test pass (candidate lists) changes scheduling, not results: identical
+    frames against the fused kernel (RT_CREATE_NO_SPLIT), also when every list overflows
+    (RT_CAND_CAP=1: overflowing pixels re-walk from scratch)."""
+    spec = {"config1": scenes.config1_spheres, "small3": lambda: scenes.small_random(3),
+            "small8": lambda: scenes.small_random(8, n_tri=800, half=0.04),
+            "config2": scenes.config2}[name]()
+    cam, cfg = scenes.make_camera(320, 200), scenes.make_config(3)
+    scene = rtamd.build_scene(spec)
+    ctx.upload(scene)
+    split = ctx.trace_frame(cam, cfg, stats=False, allow_fault=True)
+    ctxs = []
+    try:
+        fused = rtamd.Context(0, flags=abi.RT_CREATE_NO_SPLIT)
+        ctxs.append(fused)
+        fused.upload(scene)
+        _same_frames(split, fused.trace_frame(cam, cfg, stats=False, allow_fault=True))
+        monkeypatch.setenv("RT_CAND_CAP", "1")
+        tiny = rtamd.Context(0)
+        ctxs.append(tiny)
+        tiny.upload(scene)
+        _same_frames(split, tiny.trace_frame(cam, cfg, stats=False, allow_fault=True))
+    finally:
+        for c in ctxs:
+            c.close()
 
 
 def test_roughness_rejected(ctx):

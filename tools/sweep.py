@@ -1,5 +1,5 @@
 """Timing sweep of k_trace variants in one process (env knobs read at rt_create):
-RT_OCC (occupancy variant), RT_DIAG (timing-only experiments), RT_NO_CULL, RT_BVH_SAH.
+RT_OCC (occupancy variant), RT_DIAG (timing-only experiments), RT_NO_CULL, RT_BVH_SAH, RT_SPLIT, RT_CAND_CAP.
 
     python tools/sweep.py [--config config3] [--frames 5] VARIANT...   (VARIANT = "NAME:K=V,K=V")
 """
@@ -17,7 +17,7 @@ import torch  # noqa: E402,F401  (same HIP runtime as bench.py)
 import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
 
-KNOBS = ("RT_OCC", "RT_DIAG", "RT_NO_CULL", "RT_BVH_SAH")
+KNOBS = ("RT_OCC", "RT_DIAG", "RT_NO_CULL", "RT_BVH_SAH", "RT_SPLIT", "RT_CAND_CAP")
 
 
 def main():
