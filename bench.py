@@ -71,8 +71,13 @@ def cpu_baseline(spec, cam, cfg, budget_s):
                        % (done, cam.width, cam.height, segs, t_used))
 
 
+TRACE_KERNELS = ("k_walk", "k_first", "k_shade", "k_cont", "k_trace")
+PMC_FRAMES = 4                 # frames the --pmc-child run traces (warmup 1 + steps 3)
+
+
 def _pmc_pass(counter, config, stripe, timeout_s):
-    """One rocprofv3 --pmc pass over a child bench run; mean counter value per k_trace<false,*> launch."""
+    """One rocprofv3 --pmc pass over a child bench run; counter total per frame over the trace
+    kernels (the stats instantiation k_trace<true, ...> is not part of a frame)."""
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None, "rocprofv3 not on PATH"
@@ -90,14 +95,13 @@ def _pmc_pass(counter, config, stripe, timeout_s):
         for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    # the frame kernel only (the STATS instantiation is k_trace<true, ...>)
                     name = r["Kernel_Name"]
                     stats = "<true" in name or "ILb1E" in name
-                    if "k_trace" in name and not stats and r["Counter_Name"] == counter:
+                    if any(k in name for k in TRACE_KERNELS) and not stats and r["Counter_Name"] == counter:
                         vals.append(float(r["Counter_Value"]))
         if not vals:
-            return None, "%s pass: no k_trace rows in the counter CSV" % counter
-        return sum(vals) / len(vals), None
+            return None, "%s pass: no trace-kernel rows in the counter CSV" % counter
+        return sum(vals) / PMC_FRAMES, None
     except Exception as e:  # the bench line must not depend on the profiler
         return None, "%s pass: %r" % (counter, e)
     finally:
@@ -105,8 +109,8 @@ def _pmc_pass(counter, config, stripe, timeout_s):
 
 
 def hbm_traffic(config, stripe, timeout_s=300):
-    """HBM bytes per k_trace launch from PMC (MI355X_MICROARCH.md HBM section): FETCH_SIZE and
-    WRITE_SIZE in separate passes (TCC slots), both in KiB; FETCH_SIZE doubled (gfx950 tallies
+    """HBM bytes per frame's trace kernels from PMC (MI355X_MICROARCH.md HBM section): FETCH_SIZE
+    and WRITE_SIZE in separate passes (TCC slots), both in KiB; FETCH_SIZE doubled (gfx950 tallies
     128-B requests at 64 B).  None when rocprofv3 or a pass is unavailable."""
     fetch, err = _pmc_pass("FETCH_SIZE", config, stripe, timeout_s)
     if err:
@@ -115,8 +119,8 @@ def hbm_traffic(config, stripe, timeout_s=300):
     if err:
         return None, err
     return dict(bytes=2 * fetch * 1024 + write * 1024, fetch_kib_raw=fetch, write_kib=write,
-                method="rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes), per k_trace launch: "
-                       "2*FETCH_SIZE + WRITE_SIZE"), None
+                method="rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes), summed over one frame's trace "
+                       "kernels: 2*FETCH_SIZE + WRITE_SIZE"), None
 
 
 def pmc_child(args):
@@ -127,7 +131,7 @@ def pmc_child(args):
     cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
     buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
     s = torch.cuda.Stream()
-    for _ in range(args.warmup + args.steps):
+    for _ in range(PMC_FRAMES):
         ctx.trace_rows_device(cam, cfg, 0, 1, args.stripe, buf.data_ptr(), s.cuda_stream)
     s.synchronize()
     ctx.close()
@@ -213,7 +217,8 @@ def main():
     achieved = local_bytes / (k_ms * 1e-3) / 1e9 if k_ms == k_ms and k_ms > 0 else None
     roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=(achieved / HBM_PEAK_GBS) if achieved else None, traffic=None,
-                    kernel="k_trace", kernel_ms=k_ms, bytes_per_launch=local_bytes,
+                    kernel="trace (k_walk + k_first + k_shade per bounce level, k_cont)", kernel_ms=k_ms,
+                    bytes_per_launch=local_bytes,
                     bytes_formula="48*n_ret+32*n_slot+40*n_loc+32*n_cull+80*n_exact+44*n_hit+36*primary",
                     bytes_reference_equivalent=local_bytes_ref,
                     reference_equivalent_formula="SURVEY 8d: 48*n_ret+32*n_slot+40*n_loc+36*n_sph+36*n_box+76*n_tri+40*n_hit+12*primary")

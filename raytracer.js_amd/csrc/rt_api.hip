@@ -74,6 +74,8 @@ struct rt_ctx {
     bool bvh_sah = true;             // SAH splits (RT_BVH_SAH=0: median split)
     bool split = true;               // walk pass + test pass (RT_SPLIT=0: fused k_trace)
     int cand_cap = 64;               // candidate nodes per pixel in the split path (RT_CAND_CAP)
+    int cont_group = 8;              // continuation rays per wave (RT_CONT_GROUP): their passes are
+                                     // latency-bound, fewer lanes per wave shorten the slowest wave
     int occ = 0;
     int diag = 0;
     hipStream_t stream = nullptr;
@@ -113,6 +115,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_SPLIT")) c->split = atoi(e) != 0;
     if (c->flags & RT_CREATE_NO_SPLIT) c->split = false;
     if (const char *e = getenv("RT_CAND_CAP")) c->cand_cap = atoi(e) < 1 ? 1 : atoi(e);
+    if (const char *e = getenv("RT_CONT_GROUP")) c->cont_group = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     int r = use_device(c);
@@ -327,6 +330,7 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.ctr = (int32_t *)c->b_ctr.p;
     L.occ = c->occ;
     L.diag = c->diag;
+    L.cont_group = c->cont_group;
     if (c->split && P > 0) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).

@@ -102,6 +102,7 @@ struct RtLaunch {
     struct RtCont *queue[2];                    // device [rows*W] each: continuations, by level parity
     struct RtCont *ovf;                         // device [rows*W]: rays left to the fused kernel
     int32_t level, last_level;                  // set per launch by rt_launch_frame
+    int32_t cont_group;                         // continuation rays per wave (levels >= 1)
 };
 
 enum { RT_MAX_LEVELS = 32, RT_CTR_INTS = 4 + 4 * (RT_MAX_LEVELS + 1) };

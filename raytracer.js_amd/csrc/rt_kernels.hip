@@ -249,10 +249,10 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
 }
 
 // update_next_pos — :369-384 with dim_relative_to_parent :127-136.  Returns 0 or -1 (throw).
-__device__ __forceinline__ int walker_update_next_pos(const RtDevScene &S, Walker &w, Counters &c)
+// `p` = node_ps of w.cur_tree.
+__device__ __forceinline__ int walker_update_next_pos(const NodeDims &p, Walker &w, Counters &c)
 {
     c.slot++;
-    const NodeDims p = node_dims(S, w.cur_tree);
     const int n = w.cur_oct;
     const double ph = p.s / 2;
     const double dx = p.x + (double)((n >> 0) & 1) * ph;
@@ -311,7 +311,7 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
                     w.flags &= ~F_RET;
                     continue;
                 }
-                if (walker_update_next_pos(S, w, c) < 0) return -1;
+                if (walker_update_next_pos(node_dims(S, w.cur_tree), w, c) < 0) return -1;
             }
             if (!(w.nn & 16)) return -1;                     // vector.add(v, undefined)
             // cur_octant + normal: only the normal's axis can leave {0,1}
@@ -908,7 +908,8 @@ struct RaySrc {
 __device__ __forceinline__ int n_items(const RtLaunch &L)
 {
     if (L.level == 0) return ((L.cam.width + 7) >> 3) * ((L.rows + 7) >> 3);
-    return (*lvl_ctr(L, L.level - 1) + 63) >> 6;
+    const int g = L.cont_group;
+    return (*lvl_ctr(L, L.level - 1) + g - 1) / g;
 }
 
 __device__ __forceinline__ void ray_src(const RtLaunch &L, int item, int lane, RaySrc &r)
@@ -927,8 +928,8 @@ __device__ __forceinline__ void ray_src(const RtLaunch &L, int item, int lane, R
         const size_t di = (size_t)x * (size_t)L.rows + (size_t)lr;           // x-major (k_raygen)
         for (int i = 0; i < 3; i++) { r.o[i] = L.cam.pos[i]; r.d[i] = L.dirs[(size_t)i * plane + di]; }
     } else {
-        const int q = item * 64 + lane;
-        r.valid = q < *lvl_ctr(L, L.level - 1);
+        const int q = item * L.cont_group + lane;
+        r.valid = lane < L.cont_group && q < *lvl_ctr(L, L.level - 1);
         if (!r.valid) return;
         r.id = (size_t)q;
         r.rec = L.queue[(L.level - 1) & 1] + q;
