@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "raytracer.js_amd", "python"))
 
 import rtamd  # noqa: E402  (after torch: share its HIP runtime)
 from rtamd import scenes  # noqa: E402
+from rtamd import abi  # noqa: E402
 from rtamd.stripes import StripeGather  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
@@ -121,6 +122,34 @@ def hbm_traffic(config, stripe, timeout_s=300):
     return dict(bytes=2 * fetch * 1024 + write * 1024, fetch_kib_raw=fetch, write_kib=write,
                 method="rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes), summed over one frame's trace "
                        "kernels: 2*FETCH_SIZE + WRITE_SIZE"), None
+
+
+def exposure_bench(ctx, frame, stream, reps=20):
+    """The device-resident ExposureBuffer consumers on the frame just rendered:
+    luminance statistics (two read passes, synchronising) and the RGBA8 tone map (one read, one
+    write), as achieved HBM rate of their algorithmic bytes."""
+    n = frame.shape[0] * frame.shape[1]
+    sp = stream.cuda_stream
+    st = ctx.exposure_stats_device(frame.data_ptr(), n, sp)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        st = ctx.exposure_stats_device(frame.data_ptr(), n, sp)
+    stats_ms = (time.perf_counter() - t0) / reps * 1e3
+    lo, hi = rtamd.tonemap_range(abi.RT_TONEMAP_STDDEV, st)
+    rgba = torch.empty(4 * n, dtype=torch.uint8, device=frame.device)
+    ctx.tonemap_device(frame.data_ptr(), n, lo, hi, rgba.data_ptr(), sp)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        ctx.tonemap_device(frame.data_ptr(), n, lo, hi, rgba.data_ptr(), sp)
+    e1.record(stream)
+    e1.synchronize()
+    tm_ms = e0.elapsed_time(e1) / reps
+    stats_bytes, tm_bytes = 2 * 12 * n, 12 * n + 4 * n
+    return dict(stats_ms=round(stats_ms, 4), stats_GBps=round(stats_bytes / (stats_ms * 1e-3) / 1e9, 1),
+                stats_note="wall time incl. launch + 24-B readback + sync",
+                tonemap_ms=round(tm_ms, 4), tonemap_GBps=round(tm_bytes / (tm_ms * 1e-3) / 1e9, 1),
+                mean=st.mean, variance=st.variance, range=[lo, hi])
 
 
 def pmc_child(args):
@@ -237,6 +266,8 @@ def main():
         host = dict(entry="rt_trace_frame (host RGB buffer)", ms_per_frame=round(host_ms, 3),
                     value=round(tot["segments"] / (host_ms * 1e-3) / 1e6, 3), unit="Mrays/s")
 
+    exposure = exposure_bench(ctx, sg.frame, stream) if rank == 0 else None
+
     traffic = None
     if rank == 0 and world == 1 and not args.no_traffic:
         traffic, err = hbm_traffic(args.config, args.stripe)
@@ -271,6 +302,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "pcie_inclusive": host,
+            "exposure": exposure,
+            "mpixels_per_s": round(W * H * args.steps / elapsed / 1e6, 3),
         }
         print(json.dumps(rec), flush=True)
     ctx.close()

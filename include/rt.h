@@ -178,9 +178,11 @@ int  rt_trace_frame(rt_ctx *ctx, const rt_camera_desc *cam, const rt_config_desc
 
 /* Row-striped frame slice for multi-GPU: rows are grouped in stripes of `stripe_rows`; stripe s
  * belongs to part (s % n_parts).  Writes this part's rows compactly (stripe order) into the
- * DEVICE buffer d_rgb (rows_of_part * W * 3 floats, col_weight ignored: plain store) on the HIP
- * stream `stream` (NULL = the context's stream) and returns without synchronising unless
- * stats != NULL.  *rows_out = number of rows this part owns. */
+ * DEVICE buffer d_rgb (rows_of_part * W * 3 floats) on the HIP stream `stream` (NULL = the
+ * context's stream) and returns without synchronising unless stats != NULL.  With col_weight != 1
+ * the new colour is blended into d_rgb's current content exactly as rt_trace_frame does, so a
+ * progressive exposure stays device-resident across frames (ExposureBuffer.next_frame only sets
+ * col_weight = 1/(1+frame_count), src/view/exposure_buffer.ts:53-60).  *rows_out = rows owned. */
 int  rt_trace_rows_device(rt_ctx *ctx, const rt_camera_desc *cam, const rt_config_desc *cfg,
                           int32_t part, int32_t n_parts, int32_t stripe_rows,
                           void *d_rgb, void *stream, int32_t *rows_out, rt_stats *stats);
@@ -197,6 +199,34 @@ int  rt_debug_walk(rt_ctx *ctx, const double origin[3], const double dir[3], int
 /* Debug: per-pixel primary directions (W*H*3 doubles, row-major) as the ray-generation kernel
  * produced them for `cam` (Camera.get_dir_for_each_pixel, src/view/camera.ts:207-250). */
 int  rt_debug_camera_dirs(rt_ctx *ctx, const rt_camera_desc *cam, double *dirs_out);
+
+/* ---- device-resident exposure buffer: statistics and tone mapping ---- */
+typedef struct rt_exposure_stats {
+    double mean;       /* ExposureBuffer.get_mean()              src/view/exposure_buffer.ts:90-104  */
+    double variance;   /* ExposureBuffer.get_variance(mean)      src/view/exposure_buffer.ts:106-120 */
+    double absdev;     /* ExposureBuffer.get_absolute_dev(mean)  src/view/exposure_buffer.ts:122-136 */
+} rt_exposure_stats;
+
+/* Luminance statistics (Y = 0.299 R + 0.587 G + 0.114 B per pixel, in binary64) of the DEVICE
+ * buffer d_rgb (n_pixels * 3 floats).  The reference sums sequentially; the device sums in a
+ * fixed tree order; both are within n * 2^-53 (relative) of the exact sum.
+ * Synchronises `stream` (NULL = the context's stream). */
+int  rt_exposure_stats_device(rt_ctx *ctx, const float *d_rgb, int64_t n_pixels, void *stream,
+                              rt_exposure_stats *out);
+
+/* ExposureBuffer.discretize_to_screen(screen, low, high) + CanvasScreen.set_pixel_i
+ * (src/view/exposure_buffer.ts:145-158, src/view/screen_canvas.ts:45-55,92-94): the RGBA8 image
+ * (n_pixels * 4 bytes, DEVICE) a canvas would receive, bit-exact, including the reference's
+ * two-channel slice (blue is written as 0) and alpha 255.  Does not synchronise. */
+int  rt_tonemap_device(rt_ctx *ctx, const float *d_rgb, int64_t n_pixels, double drange_low, double drange_high,
+                       uint8_t *d_rgba, void *stream);
+
+/* ToneMapper.get_dynamic_range (src/view/tone_mapping.ts:22-80) from statistics: [low, high]. */
+#define RT_TONEMAP_IDENTITY 0   /* ToneMapper_Identity:        [0, 1]                          */
+#define RT_TONEMAP_STDDEV   1   /* ToneMapper_StdDevAroundMean: mean + sqrt(variance)          */
+#define RT_TONEMAP_ABSDEV   2   /* ToneMapper_AbsDevAroundMean: mean + absdev                  */
+int  rt_tonemap_range(int32_t mode, const rt_exposure_stats *st, int32_t dynamic_range, double min_dynamic,
+                      double max_dynamic, double range_out[2]);
 
 /* ---- host-side scene builder (native add_entity_to_octree, src/octree_entity.ts:60-188) ---- */
 typedef struct rt_builder rt_builder;

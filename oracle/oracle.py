@@ -57,6 +57,12 @@ def lib():
     L.orc_linear_size.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.orc_linearize.argtypes = [vp, pd, pd, pi, pi, pi, pi, pi]
     L.orc_camera_dirs.argtypes = [C.POINTER(abi.rt_camera_desc), pd]
+    pf = C.POINTER(C.c_float)
+    L.orc_exposure_stats.argtypes = [pf, C.c_int64, pd]
+    L.orc_exposure_stats.restype = None
+    L.orc_tonemap_range.argtypes = [i, pd, i, C.c_double, C.c_double, pd]
+    L.orc_tonemap.argtypes = [pf, C.c_int64, C.c_double, C.c_double, C.POINTER(C.c_uint8)]
+    L.orc_tonemap.restype = None
     L.orc_camera_scan_literal.argtypes = [C.POINTER(abi.rt_camera_desc), pi, pi, pd]
     L.orc_trace_frame.argtypes = [vp, vp, C.POINTER(abi.rt_camera_desc), C.POINTER(abi.rt_config_desc),
                                   i, pi, C.POINTER(C.c_float), pi, pi, pi, C.POINTER(C.c_uint8),
@@ -243,3 +249,32 @@ def build_scene(spec):
     w.set_tables(spec.shades, spec.substances)
     w.add_entities(root, spec.entities)
     return w, root
+
+
+# ---- ExposureBuffer consumers (src/view/exposure_buffer.ts, src/view/tone_mapping.ts) ----------------
+def exposure_stats(rgb):
+    """{mean, variance, absdev} of a W*H*3 float32 buffer (sequential sums, as the reference)."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    out = np.zeros(3)
+    lib().orc_exposure_stats(rgb.ctypes.data_as(C.POINTER(C.c_float)), len(rgb) // 3,
+                             out.ctypes.data_as(C.POINTER(C.c_double)))
+    return out
+
+
+def tonemap_range(mode, stats, dynamic_range=8, min_dynamic=1.0 / 256, max_dynamic=8.0):
+    st = np.ascontiguousarray(stats, dtype=np.float64)
+    out = np.zeros(2)
+    if lib().orc_tonemap_range(int(mode), st.ctypes.data_as(C.POINTER(C.c_double)), int(dynamic_range),
+                               float(min_dynamic), float(max_dynamic), out.ctypes.data_as(C.POINTER(C.c_double))):
+        raise ValueError("bad tone-mapper mode %r" % mode)
+    return out
+
+
+def tonemap(rgb, low, high):
+    """RGBA8 (n_pixels*4 uint8) a CanvasScreen receives from discretize_to_screen."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    n = len(rgb) // 3
+    out = np.zeros(4 * n, np.uint8)
+    lib().orc_tonemap(rgb.ctypes.data_as(C.POINTER(C.c_float)), n, float(low), float(high),
+                      out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out

@@ -1176,3 +1176,78 @@ int orc_trace_frame(oworld *w, onode *root, const rt_camera_desc *cam, const rt_
     free(dirs);
     return tot[10] ? ORC_FAULT : 0;
 }
+
+/* ============================ ExposureBuffer consumers ===================================== */
+
+/* rgb_to_y, src/view/exposure_buffer.ts:161-172: W_R*r + W_G*g + W_B*b, left to right */
+static double orc_rgb_to_y(const float *px)
+{
+    const double W_R = 0.299, W_G = 0.587, W_B = 0.114;
+    return W_R * (double)px[0] + W_G * (double)px[1] + W_B * (double)px[2];
+}
+
+/* get_mean :90-104, get_variance(mean) :106-120, get_absolute_dev(mean) :122-136 — sequential
+ * sums, each divided by n_pixels (the _mean/_variance caches are never filled). */
+void orc_exposure_stats(const float *rgb, int64_t n_pixels, double out[3])
+{
+    double mean = 0;
+    for (int64_t i = 0; i < n_pixels * 3; i += 3) mean += orc_rgb_to_y(rgb + i);
+    mean /= (double)n_pixels;
+    double variance = 0;
+    for (int64_t i = 0; i < n_pixels * 3; i += 3) {
+        const double delta = orc_rgb_to_y(rgb + i) - mean;
+        variance += delta * delta;
+    }
+    variance /= (double)n_pixels;
+    double dev = 0;
+    for (int64_t i = 0; i < n_pixels * 3; i += 3) dev += fabs(orc_rgb_to_y(rgb + i) - mean);
+    dev /= (double)n_pixels;
+    out[0] = mean;
+    out[1] = variance;
+    out[2] = dev;
+}
+
+/* clamp, src/math/mathutils.ts:18-20 */
+static double js_clamp(double x, double lo, double hi) { return js_max(js_min(x, hi), lo); }
+
+/* ToneMapper_Identity :26-34; ToneMapper_DRLimited constructor :39-44 (dynamic_coef = 1 << dr);
+ * _StdDevAroundMean :48-63; _AbsDevAroundMean :65-80 */
+int orc_tonemap_range(int mode, const double stats[3], int dynamic_range, double min_dynamic, double max_dynamic,
+                      double out[2])
+{
+    if (mode == 0) { out[0] = 0; out[1] = 1; return 0; }
+    if (mode != 1 && mode != 2) return -1;
+    const double coef = (double)(int32_t)((uint32_t)1 << ((uint32_t)dynamic_range & 31));
+    const double mean_br = stats[0];
+    const double dev_br = mode == 1 ? sqrt(stats[1]) : stats[2];
+    double drange_max = js_min(mean_br + dev_br, max_dynamic);
+    double drange_min = drange_max / coef;
+    if (drange_min < min_dynamic) {
+        drange_min = min_dynamic;
+        drange_max = drange_min * coef;
+    }
+    out[0] = drange_min;
+    out[1] = drange_max;
+    return 0;
+}
+
+/* discretize_to_screen :145-158 with CanvasScreen.set_pixel_i / convert_color
+ * (src/view/screen_canvas.ts:45-55,92-94).  `this.pixels.slice(i, i+2)` is a two-element
+ * Float32Array; its .map() stores each clamp(c * scale_coef, 0, 1) rounded to f32, and
+ * convert_color maps those through (clamp(x,0,1)*255) << 0.  col_conv[2] is undefined, which the
+ * Uint8ClampedArray stores as 0; alpha is 0xff. */
+void orc_tonemap(const float *rgb, int64_t n_pixels, double low, double high, uint8_t *rgba)
+{
+    const double drange = high - low;
+    const double EPS = 2.220446049250313e-16;          /* Number.EPSILON */
+    for (int64_t px_i = 0, i = 0; px_i < n_pixels; ++px_i, i += 3) {
+        const double px_brightness = orc_rgb_to_y(rgb + i);
+        const double cmpr_brightness = (px_brightness - low) / drange;
+        const double scale_coef = cmpr_brightness / (px_brightness + EPS);
+        float compressed[2];
+        for (int k = 0; k < 2; k++) compressed[k] = (float)js_clamp((double)rgb[i + k] * scale_coef, 0.0, 1.0);
+        for (int k = 0; k < 2; k++) rgba[4 * px_i + k] = (uint8_t)js_toint32(js_clamp((double)compressed[k], 0.0, 1.0) * 255);
+        rgba[4 * px_i + 2] = 0;
+        rgba[4 * px_i + 3] = 0xff;
+    }
+}

@@ -85,6 +85,15 @@ int  orc_trace_frame(oworld *w, onode *root, const rt_camera_desc *cam, const rt
                      int32_t *hit_node, int32_t *segments, uint8_t *status, int64_t *counters,
                      int nthreads);
 
+/* ExposureBuffer consumers (src/view/exposure_buffer.ts, src/view/tone_mapping.ts,
+ * src/view/screen_canvas.ts): sequential luminance statistics {mean, variance, absdev}, the
+ * ToneMapper dynamic range (mode 0 identity, 1 std-dev, 2 abs-dev), and the RGBA8 image
+ * discretize_to_screen hands a CanvasScreen. */
+void orc_exposure_stats(const float *rgb, int64_t n_pixels, double out[3]);
+int  orc_tonemap_range(int mode, const double stats[3], int dynamic_range, double min_dynamic,
+                       double max_dynamic, double out[2]);
+void orc_tonemap(const float *rgb, int64_t n_pixels, double low, double high, uint8_t *rgba);
+
 #ifdef __cplusplus
 }
 #endif

@@ -84,7 +84,7 @@ struct rt_ctx {
     RtDevScene scene{};
     DevBuf b_node_ps, b_node_child, b_node_up, b_node_ent, b_prim, b_shades, b_ent_sub, b_sub_ri;
     DevBuf b_bvh, b_list, b_prefix;
-    DevBuf b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_fr, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
+    DevBuf b_stat, b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_fr, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
     DevBuf b_walk;
     static constexpr int NEV = 256;
     hipEvent_t ev[NEV][2] = {};
@@ -142,7 +142,7 @@ extern "C" void rt_destroy(rt_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->b_node_ps, &c->b_node_child, &c->b_node_up, &c->b_node_ent, &c->b_prim,
-                      &c->b_shades, &c->b_ent_sub, &c->b_sub_ri, &c->b_cand, &c->b_cand_n, &c->b_first, &c->b_queue, &c->b_ctr, &c->b_setup, &c->b_fr, &c->b_dirs,
+                      &c->b_shades, &c->b_ent_sub, &c->b_sub_ri, &c->b_stat, &c->b_cand, &c->b_cand_n, &c->b_first, &c->b_queue, &c->b_ctr, &c->b_setup, &c->b_fr, &c->b_dirs,
                       &c->b_rgb, &c->b_hit_e, &c->b_hit_n, &c->b_status, &c->b_counters, &c->b_fault,
                       &c->b_walk, &c->b_bvh, &c->b_list, &c->b_prefix};
     for (DevBuf *b : bufs) b->release();
@@ -424,7 +424,7 @@ extern "C" int rt_trace_rows_device(rt_ctx *c, const rt_camera_desc *cam, const 
     if (!d_rgb && L.rows > 0) return rt_set_error(RT_E_INVALID, "rt_trace_rows_device: d_rgb is null");
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     L.rgb = (float *)d_rgb;
-    L.blend = 0;
+    L.blend = cfg->col_weight != 1.0;
     if (stats) {
         HIP_TRY(hipMemsetAsync(c->b_counters.p, 0, sizeof(unsigned long long) * CT_N, st));
         L.counters = (unsigned long long *)c->b_counters.p;
@@ -444,6 +444,66 @@ extern "C" int rt_trace_rows_device(rt_ctx *c, const rt_camera_desc *cam, const 
         stats->kernel_ms = ms;
         stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
+    return RT_OK;
+}
+
+// ---- device-resident exposure buffer (rt_exposure.hip) ---------------------------------
+extern "C" int rt_exposure_stats_device(rt_ctx *c, const float *d_rgb, int64_t n_pixels, void *stream,
+                                        rt_exposure_stats *out)
+{
+    if (!c || !out || n_pixels < 0 || (n_pixels > 0 && !d_rgb))
+        return rt_set_error(RT_E_INVALID, "rt_exposure_stats_device: bad argument");
+    int r = use_device(c);
+    if (r != RT_OK) return r;
+    const int n_blocks = (int)(n_pixels / 256 + 1 < 1024 ? n_pixels / 256 + 1 : 1024);
+    if ((r = c->b_stat.ensure(sizeof(double) * (2 * (size_t)n_blocks + 4))) != RT_OK) return r;
+    double *d_out = (double *)c->b_stat.p;
+    double *d_part = d_out + 4;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if ((r = rt_launch_exposure_stats(d_rgb, (long long)n_pixels, d_part, n_blocks, d_out, st)) != RT_OK) return r;
+    double h[3];
+    HIP_TRY(hipMemcpyAsync(h, d_out, sizeof h, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    out->mean = h[0];
+    out->variance = h[1];
+    out->absdev = h[2];
+    return RT_OK;
+}
+
+extern "C" int rt_tonemap_device(rt_ctx *c, const float *d_rgb, int64_t n_pixels, double drange_low,
+                                 double drange_high, uint8_t *d_rgba, void *stream)
+{
+    if (!c || n_pixels < 0 || (n_pixels > 0 && (!d_rgb || !d_rgba)))
+        return rt_set_error(RT_E_INVALID, "rt_tonemap_device: bad argument");
+    int r = use_device(c);
+    if (r != RT_OK) return r;
+    return rt_launch_tonemap(d_rgb, (long long)n_pixels, drange_low, drange_high, d_rgba,
+                             stream ? (hipStream_t)stream : c->stream);
+}
+
+// ToneMapper_DRLimited / _StdDevAroundMean / _AbsDevAroundMean / _Identity (src/view/tone_mapping.ts:22-80)
+extern "C" int rt_tonemap_range(int32_t mode, const rt_exposure_stats *st, int32_t dynamic_range, double min_dynamic,
+                                double max_dynamic, double range_out[2])
+{
+    if (!range_out || (mode != RT_TONEMAP_IDENTITY && !st))
+        return rt_set_error(RT_E_INVALID, "rt_tonemap_range: null argument");
+    if (mode == RT_TONEMAP_IDENTITY) {
+        range_out[0] = 0;
+        range_out[1] = 1;
+        return RT_OK;
+    }
+    if (mode != RT_TONEMAP_STDDEV && mode != RT_TONEMAP_ABSDEV)
+        return rt_set_error(RT_E_INVALID, "rt_tonemap_range: mode %d", mode);
+    const double coef = (double)(int32_t)(1u << ((uint32_t)dynamic_range & 31));   // 1 << dynamic_range
+    const double dev = mode == RT_TONEMAP_STDDEV ? sqrt(st->variance) : st->absdev;
+    double hi = rtjs::jmin(st->mean + dev, max_dynamic);
+    double lo = hi / coef;
+    if (lo < min_dynamic) {
+        lo = min_dynamic;
+        hi = lo * coef;
+    }
+    range_out[0] = lo;
+    range_out[1] = hi;
     return RT_OK;
 }
 

@@ -108,6 +108,10 @@ struct RtLaunch {
 enum { RT_MAX_LEVELS = 32, RT_CTR_INTS = 4 + 4 * (RT_MAX_LEVELS + 1) };
 
 int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end);
+// rt_exposure.hip: statistics into d_out3 = {mean, variance, absdev} (d_partials: 2 * n_blocks doubles)
+int rt_launch_exposure_stats(const float *d_rgb, long long n, double *d_partials, int n_blocks, double *d_out3,
+                             void *stream);
+int rt_launch_tonemap(const float *d_rgb, long long n, double low, double high, uint8_t *d_rgba, void *stream);
 int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[3], int include_undefined,
                          int max_out, int32_t *d_tree, int32_t *d_oct, int32_t *d_n, void *stream);
 

@@ -29,6 +29,12 @@ def load_library(path=None):
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
+    try:
+        # torch bundles its own HIP runtime: it must initialise before librt_amd.so pulls in the
+        # system one, or torch later finds no device in this process
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(p):
         raise RuntimeError("librt_amd.so not found at %s — run __graft_entry__.build() (make -C raytracer.js_amd)" % p)
     lib = abi.declare(C.CDLL(p))
@@ -163,6 +169,18 @@ class Context:
             _check(rc)
         return dict(rgb=rgb, hit_entity=he, hit_node=hn, status=st, stats=s, rc=rc)
 
+    def exposure_stats_device(self, d_rgb_ptr, n_pixels, stream_ptr=None):
+        """ExposureBuffer.get_mean / get_variance / get_absolute_dev of a device buffer (synchronises)."""
+        out = abi.rt_exposure_stats()
+        _check(self.L.rt_exposure_stats_device(self.h, C.c_void_p(d_rgb_ptr), int(n_pixels),
+                                               C.c_void_p(stream_ptr) if stream_ptr else None, C.byref(out)))
+        return out
+
+    def tonemap_device(self, d_rgb_ptr, n_pixels, low, high, d_rgba_ptr, stream_ptr=None):
+        """discretize_to_screen + CanvasScreen conversion into a device RGBA8 buffer (asynchronous)."""
+        _check(self.L.rt_tonemap_device(self.h, C.c_void_p(d_rgb_ptr), int(n_pixels), float(low), float(high),
+                                        C.c_void_p(d_rgba_ptr), C.c_void_p(stream_ptr) if stream_ptr else None))
+
     def trace_rows_device(self, cam, cfg, part, n_parts, stripe, d_rgb_ptr, stream_ptr=None, stats=False):
         rows = C.c_int32()
         s = abi.rt_stats() if stats else None
@@ -196,3 +214,11 @@ def part_rows(H, part, n_parts, stripe):
     """Global row indices owned by `part` in stripe order (mirrors rt_part_rows)."""
     from .stripes import part_rows as _pr
     return _pr(H, part, n_parts, stripe)
+
+
+def tonemap_range(mode, stats, dynamic_range=8, min_dynamic=1.0 / 256, max_dynamic=8.0):
+    """ToneMapper.get_dynamic_range (src/view/tone_mapping.ts:22-80) from rt_exposure_stats (host)."""
+    out = np.zeros(2)
+    _check(load_library().rt_tonemap_range(int(mode), C.byref(stats), int(dynamic_range), float(min_dynamic),
+                                           float(max_dynamic), out.ctypes.data_as(C.POINTER(C.c_double))))
+    return out

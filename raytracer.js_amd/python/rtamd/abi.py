@@ -78,6 +78,13 @@ class rt_stats(C.Structure):
         return {k: int(getattr(self, k)) for k in self.WORK}
 
 
+class rt_exposure_stats(C.Structure):
+    _fields_ = [("mean", _d), ("variance", _d), ("absdev", _d)]
+
+
+RT_TONEMAP_IDENTITY, RT_TONEMAP_STDDEV, RT_TONEMAP_ABSDEV = 0, 1, 2
+
+
 class rt_create_desc(C.Structure):
     _fields_ = [("device", _i), ("flags", _i)]
 
@@ -96,7 +103,8 @@ assert ENTITY_DTYPE.itemsize == C.sizeof(rt_entity_in)
 EXPORTS = ("rt_create", "rt_destroy", "rt_last_error", "rt_abi_version", "rt_upload_scene",
            "rt_trace_frame", "rt_trace_rows_device", "rt_kernel_times", "rt_debug_walk",
            "rt_debug_camera_dirs", "rt_builder_create", "rt_builder_destroy", "rt_builder_add",
-           "rt_builder_add_many", "rt_builder_desc")
+           "rt_builder_add_many", "rt_builder_desc", "rt_exposure_stats_device", "rt_tonemap_device",
+           "rt_tonemap_range")
 
 
 def declare(lib):
@@ -122,6 +130,9 @@ def declare(lib):
     lib.rt_builder_add.argtypes = [vp, P(rt_entity_in), _pi]
     lib.rt_builder_add_many.argtypes = [vp, P(rt_entity_in), _i]
     lib.rt_builder_desc.argtypes = [vp, P(rt_shade), _i, _pd, _i, P(rt_scene_desc)]
+    lib.rt_exposure_stats_device.argtypes = [vp, vp, C.c_int64, vp, P(rt_exposure_stats)]
+    lib.rt_tonemap_device.argtypes = [vp, vp, C.c_int64, _d, _d, vp, vp]
+    lib.rt_tonemap_range.argtypes = [_i, P(rt_exposure_stats), _i, _d, _d, _pd]
     return lib
 
 

@@ -35,15 +35,16 @@ def test_library_exports_every_symbol():
 
 def test_struct_layouts_match_header(tmp_path):
     prog = tmp_path / "sz.c"
-    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rt.h"\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n",'
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rt.h"\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n",'
                     'sizeof(rt_shade),sizeof(rt_scene_desc),sizeof(rt_camera_desc),sizeof(rt_config_desc),'
-                    'sizeof(rt_stats),sizeof(rt_create_desc),sizeof(rt_entity_in),offsetof(rt_scene_desc,substance_ri));return 0;}\n')
+                    'sizeof(rt_stats),sizeof(rt_create_desc),sizeof(rt_entity_in),offsetof(rt_scene_desc,substance_ri),'
+                    'sizeof(rt_exposure_stats));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [C.sizeof(abi.rt_shade), C.sizeof(abi.rt_scene_desc), C.sizeof(abi.rt_camera_desc),
             C.sizeof(abi.rt_config_desc), C.sizeof(abi.rt_stats), C.sizeof(abi.rt_create_desc),
-            C.sizeof(abi.rt_entity_in), abi.rt_scene_desc.substance_ri.offset]
+            C.sizeof(abi.rt_entity_in), abi.rt_scene_desc.substance_ri.offset, C.sizeof(abi.rt_exposure_stats)]
     assert got == want
 
 
@@ -53,6 +54,8 @@ def test_null_arguments_are_rejected_without_gpu():
     assert b"null" in lib.rt_last_error()
     assert lib.rt_upload_scene(None, None) == abi.RT_E_INVALID
     assert lib.rt_trace_frame(None, None, None, None, None, None, None, None) == abi.RT_E_INVALID
+    assert lib.rt_exposure_stats_device(None, None, 0, None, None) == abi.RT_E_INVALID
+    assert lib.rt_tonemap_device(None, None, 1, 0.0, 1.0, None, None) == abi.RT_E_INVALID
 
 
 def test_missing_library_fails_loudly(tmp_path):
