@@ -218,11 +218,22 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
                 if (e < u2) { u2 = e; i2 = fe[a]; }
             }
         } else {
+            const bool s0 = ae[0] <= m + tol, s1 = ae[1] <= m + tol, s2 = ae[2] <= m + tol;   // NaN never survives
+            if ((int)s0 + (int)s1 + (int)s2 == 1) {
+                // the common case: one survivor, selected without branching so that every lane of the
+                // wave shares a single division whichever face it leaves through
+                const double q = s0 ? qe[0] : (s1 ? qe[1] : qe[2]);
+                const double pp = s0 ? pe[0] : (s1 ? pe[1] : pe[2]);
+                const int f = s0 ? fe[0] : (s1 ? fe[1] : fe[2]);
+                const double e = q / pp;
+                if (e < u2) { u2 = e; i2 = f; }
+            } else {
 #pragma unroll
-            for (int a = 0; a < 3; a++) {
-                if (ae[a] <= m + tol) {                   // survivor (NaN never survives)
-                    const double e = qe[a] / pe[a];
-                    if (e < u2) { u2 = e; i2 = fe[a]; }
+                for (int a = 0; a < 3; a++) {
+                    if (ae[a] <= m + tol) {
+                        const double e = qe[a] / pe[a];
+                        if (e < u2) { u2 = e; i2 = fe[a]; }
+                    }
                 }
             }
         }
