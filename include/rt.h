@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2   /* 2: rt_config_desc gained scatter_seed / scatter_mode */
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define RT_OK             0
@@ -121,7 +121,21 @@ typedef struct rt_config_desc {
     double  sky_rgb[3];                 /* SkySphere(SolidTexture) colour          */
     double  distance_attenuation_factor;
     double  col_weight;                 /* 1.0 after reset_exposure()              */
+    uint64_t scatter_seed;              /* RT_SCATTER_COUNTER: key of this frame's draws          */
+    int32_t scatter_mode;               /* RT_SCATTER_*                                           */
+    int32_t pad_;
 } rt_config_desc;
+
+/* Rough mirrors (roughness_index > 0): scatter_ray (src/raytracer.ts:121-133) draws from the
+ * Raytracer's one sequential FpLcg, an order-dependent stream no parallel trace can reproduce.
+ *   RT_SCATTER_REJECT   such scenes return RT_E_UNSUPPORTED (the parity gate);
+ *   RT_SCATTER_COUNTER  scatter_ray's algorithm (isotropic_sphere_sample's rejection loop, normal
+ *                       flip, blend, normalize) with draw n of the ray through pixel p (global
+ *                       index y*W+x) = (mix64(seed + p*0x9E3779B97F4A7C15 + (n+1)*0xD1B54A32D192ED03)
+ *                       >> 11) * 2^-53, mix64 = the splitmix64 finaliser.  Independent of
+ *                       scheduling and partitioning; the oracle implements the same stream. */
+#define RT_SCATTER_REJECT  0
+#define RT_SCATTER_COUNTER 1
 
 /* Work counters and timing.  Filled when a non-NULL rt_stats* is passed. */
 typedef struct rt_stats {

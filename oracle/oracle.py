@@ -63,6 +63,10 @@ def lib():
     L.orc_tonemap_range.argtypes = [i, pd, i, C.c_double, C.c_double, pd]
     L.orc_tonemap.argtypes = [pf, C.c_int64, C.c_double, C.c_double, C.POINTER(C.c_uint8)]
     L.orc_tonemap.restype = None
+    L.orc_counter_draw_at.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
+    L.orc_counter_draw_at.restype = C.c_double
+    L.orc_scatter_dir.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, pd, C.c_double, pd]
+    L.orc_scatter_dir.restype = C.c_uint32
     L.orc_camera_scan_literal.argtypes = [C.POINTER(abi.rt_camera_desc), pi, pi, pd]
     L.orc_trace_frame.argtypes = [vp, vp, C.POINTER(abi.rt_camera_desc), C.POINTER(abi.rt_config_desc),
                                   i, pi, C.POINTER(C.c_float), pi, pi, pi, C.POINTER(C.c_uint8),
@@ -278,3 +282,18 @@ def tonemap(rgb, low, high):
     lib().orc_tonemap(rgb.ctypes.data_as(C.POINTER(C.c_float)), n, float(low), float(high),
                       out.ctypes.data_as(C.POINTER(C.c_uint8)))
     return out
+
+
+def counter_draw(seed, pixel, n):
+    """Draw n of pixel `pixel` in the RT_SCATTER_COUNTER stream (include/rt.h)."""
+    return lib().orc_counter_draw_at(int(seed) & (2 ** 64 - 1), int(pixel), int(n))
+
+
+def scatter_dir(seed, pixel, draws, normal, roughness, d):
+    """One Ray.scatter_ray (src/raytracer.ts:121-133) from draw `draws`: (new direction, next draw)."""
+    nn = np.ascontiguousarray(normal, dtype=np.float64)
+    dd = np.array(d, dtype=np.float64)
+    nxt = lib().orc_scatter_dir(int(seed) & (2 ** 64 - 1), int(pixel), int(draws),
+                                nn.ctypes.data_as(C.POINTER(C.c_double)), float(roughness),
+                                dd.ctypes.data_as(C.POINTER(C.c_double)))
+    return dd, nxt

@@ -973,8 +973,57 @@ typedef struct ray_out {
     int64_t n_sph, n_box, n_tri, n_hit;
 } ray_out;
 
-static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], ray_out *ro)
+/* RT_SCATTER_COUNTER (include/rt.h): draw n of pixel p is a pure function of (seed, p, n) —
+ * the splitmix64 finaliser, top 53 bits scaled by 2^-53 — replacing the reference's shared
+ * sequential `this.tracer.rng` stream, whose draw order depends on the pixel visiting order. */
+static uint64_t orc_mix64(uint64_t z)
 {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static double orc_counter_draw(uint64_t seed, uint64_t pixel, uint32_t n)
+{
+    uint64_t x = orc_mix64(seed + pixel * 0x9E3779B97F4A7C15ULL + ((uint64_t)n + 1) * 0xD1B54A32D192ED03ULL);
+    return (double)(x >> 11) * (1.0 / 9007199254740992.0);
+}
+
+/* Ray.scatter_ray (src/raytracer.ts:121-133) after reflect_ray: isotropic_sphere_sample
+ * (src/math/vector_utils.ts:8-14, rejection sampling, x/y/z drawn in argument order; capped at 64
+ * attempts so a counter stream always terminates — P(64 rejections) = (1-pi/6)^64 ~ 1e-21), the
+ * sample flipped into the normal's hemisphere, blended with the mirror direction by
+ * roughness_index and normalised (vector.normalize_self = scale_self(v, 1.0/length(v))). */
+static void orc_scatter(uint64_t seed, uint64_t pixel, uint32_t *draws, const double n[3], double rough,
+                        double d[3])
+{
+    double v[3];
+    for (int attempt = 0;; attempt++) {
+        for (int i = 0; i < 3; i++) v[i] = orc_counter_draw(seed, pixel, (*draws)++) * 2 - 1;
+        if (!(vdot(v, v) > 1) || attempt == 63) break;
+    }
+    if (vdot(v, n) < 0)
+        for (int i = 0; i < 3; i++) v[i] *= -1;
+    double keep = 1 - rough;
+    double ref[3];
+    for (int i = 0; i < 3; i++) ref[i] = d[i] * keep + v[i] * rough;
+    double inv = 1.0 / sqrt(vdot(ref, ref));
+    for (int i = 0; i < 3; i++) d[i] = ref[i] * inv;
+}
+
+/* test hook: one scatter_ray with the counter stream; returns the draw counter after it */
+uint32_t orc_scatter_dir(uint64_t seed, uint64_t pixel, uint32_t draws, const double normal[3], double roughness,
+                         double dir_inout[3])
+{
+    orc_scatter(seed, pixel, &draws, normal, roughness, dir_inout);
+    return draws;
+}
+
+double orc_counter_draw_at(uint64_t seed, uint64_t pixel, uint32_t n) { return orc_counter_draw(seed, pixel, n); }
+
+static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], uint64_t pixel, ray_out *ro)
+{
+    uint32_t draws = 0;
     oworld *w = tc->w;
     const rt_config_desc *cfg = tc->cfg;
     double o[3] = {tc->start_pos[0], tc->start_pos[1], tc->start_pos[2]};   /* refpoint = clone(start) */
@@ -1025,7 +1074,10 @@ static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], ra
             double ns = -vdot(d, h.normal);
             double k = ns * 2;
             for (int i = 0; i < 3; i++) d[i] = d[i] + h.normal[i] * k;
-            if (sh->roughness > 0.0) { ro->status = ST_FAULT; goto out; }  /* outside the parity gate */
+            if (sh->roughness > 0.0) {                          /* :233-235 */
+                if (cfg->scatter_mode != RT_SCATTER_COUNTER) { ro->status = ST_FAULT; goto out; }
+                orc_scatter(cfg->scatter_seed, pixel, &draws, h.normal, sh->roughness, d);
+            }
             for (int i = 0; i < 3; i++) o[i] += d[i] * 1e-3;    /* move_slightly_forward :158-164 */
         } else if (sh->response == RT_RESP_TRANSMISSION) {
             for (int i = 0; i < 3; i++) o[i] += d[i] * 1e-3;
@@ -1097,7 +1149,7 @@ static void *frame_worker(void *arg)
         int p = j->pix ? j->pix[k] : k;
         ray_out ro;
         memset(&ro, 0, sizeof ro);
-        trace_ray(j->tc, j->wk, j->dirs + 3 * (size_t)p, &ro);
+        trace_ray(j->tc, j->wk, j->dirs + 3 * (size_t)p, (uint64_t)p, &ro);
         /* ExposureBuffer.set_color_i — src/view/exposure_buffer.ts:77-91 */
         float *px = j->rgb + 3 * (size_t)p;
         for (int c = 0; c < 3; c++) {

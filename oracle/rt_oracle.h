@@ -94,6 +94,12 @@ int  orc_tonemap_range(int mode, const double stats[3], int dynamic_range, doubl
                        double max_dynamic, double out[2]);
 void orc_tonemap(const float *rgb, int64_t n_pixels, double low, double high, uint8_t *rgba);
 
+/* RT_SCATTER_COUNTER (include/rt.h): draw n of pixel p, and one Ray.scatter_ray
+ * (src/raytracer.ts:121-133) on dir_inout starting at draw `draws`; returns the next draw index. */
+double orc_counter_draw_at(uint64_t seed, uint64_t pixel, uint32_t n);
+uint32_t orc_scatter_dir(uint64_t seed, uint64_t pixel, uint32_t draws, const double normal[3], double roughness,
+                         double dir_inout[3]);
+
 #ifdef __cplusplus
 }
 #endif

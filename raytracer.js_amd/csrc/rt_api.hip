@@ -290,10 +290,13 @@ static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_confi
         return rt_set_error(RT_E_INVALID, "bad screen size %dx%d", cam->width, cam->height);
     if (cfg->default_substance < -1 || cfg->default_substance >= c->scene.n_subs)
         return rt_set_error(RT_E_INVALID, "bad default_substance %d", cfg->default_substance);
-    if (c->scatter)
+    if (cfg->scatter_mode != RT_SCATTER_REJECT && cfg->scatter_mode != RT_SCATTER_COUNTER)
+        return rt_set_error(RT_E_INVALID, "bad scatter_mode %d", cfg->scatter_mode);
+    if (c->scatter && cfg->scatter_mode != RT_SCATTER_COUNTER)
         return rt_set_error(RT_E_UNSUPPORTED,
                             "roughness_index > 0 on a mirror: scatter_ray draws from one sequential PRNG "
-                            "(src/raytracer.ts:121-133) and is outside the GPU path");
+                            "(src/raytracer.ts:121-133); pass scatter_mode RT_SCATTER_COUNTER for the "
+                            "per-pixel counter stream");
     return RT_OK;
 }
 

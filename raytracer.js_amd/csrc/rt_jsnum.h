@@ -67,6 +67,19 @@ RT_HD double dot3(double a0, double a1, double a2, double b0, double b1, double 
     return s;
 }
 
+// RT_SCATTER_COUNTER draws (include/rt.h): the splitmix64 finaliser over (seed, pixel, draw).
+RT_HD uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+RT_HD double counter_draw(uint64_t seed, uint64_t pixel, uint32_t n)
+{
+    const uint64_t x = mix64(seed + pixel * 0x9E3779B97F4A7C15ULL + ((uint64_t)n + 1) * 0xD1B54A32D192ED03ULL);
+    return (double)(x >> 11) * 1.1102230246251565e-16;   // 2^-53
+}
+
 // (z << 2) + (y << 1) + (x << 0) on ToInt32 values (src/octree_space.ts:82,124).
 RT_HD double octant_sum(int32_t x, int32_t y, int32_t z)
 {

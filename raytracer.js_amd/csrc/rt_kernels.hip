@@ -694,7 +694,7 @@ struct RayQueues {
 
 __device__ __forceinline__ void queue_push(RtCont *q, int32_t *qn, const double o[3], const double d[3], double col0,
                                            double col1, double col2, double path, int refcount, int cur_sub,
-                                           const RayResult &R, int pix, int fresh)
+                                           const RayResult &R, int pix, int fresh, uint32_t draws)
 {
     const int k = atomicAdd(qn, 1);
     RtCont &e = q[k];
@@ -705,7 +705,37 @@ __device__ __forceinline__ void queue_push(RtCont *q, int32_t *qn, const double 
     e.hit_ent = R.hit_ent; e.hit_node = R.hit_node; e.segments = R.segments;
     e.pix = pix;
     e.pad[0] = fresh;
-    e.pad[1] = 0;
+    e.pad[1] = (int32_t)draws;
+}
+
+// RT_SCATTER_COUNTER key: the full-frame pixel index y*W + x of part-local pixel `pix`.
+__device__ __forceinline__ uint64_t frame_pixel(const RtLaunch &L, int pix)
+{
+    const int W = L.cam.width;
+    const int lr = pix / W;
+    return (uint64_t)part_row_to_y(lr, L.part, L.n_parts, L.stripe_rows) * (uint64_t)W + (uint64_t)(pix - lr * W);
+}
+
+// Ray.scatter_ray (src/raytracer.ts:121-133) with counter draws (include/rt.h RT_SCATTER_COUNTER):
+// isotropic_sphere_sample's rejection loop (src/math/vector_utils.ts:8-14, capped at 64 attempts),
+// the hemisphere flip, d*(1-r) + v*r and normalize_self (scale by 1.0/length).  Same operation
+// order as oracle/rt_oracle.c orc_scatter.
+__device__ __forceinline__ void scatter_dir(uint64_t seed, uint64_t gpix, uint32_t &draws, const double n[3],
+                                         double rough, double d[3])
+{
+    double v0, v1, v2;
+    for (int attempt = 0;; attempt++) {
+        v0 = rtjs::counter_draw(seed, gpix, draws) * 2 - 1;
+        v1 = rtjs::counter_draw(seed, gpix, draws + 1) * 2 - 1;
+        v2 = rtjs::counter_draw(seed, gpix, draws + 2) * 2 - 1;
+        draws += 3;
+        if (!(dot3(v0, v1, v2, v0, v1, v2) > 1) || attempt == 63) break;
+    }
+    if (dot3(v0, v1, v2, n[0], n[1], n[2]) < 0) { v0 *= -1; v1 *= -1; v2 *= -1; }
+    const double keep = 1 - rough;
+    const double r0 = d[0] * keep + v0 * rough, r1 = d[1] * keep + v1 * rough, r2 = d[2] * keep + v2 * rough;
+    const double inv = 1.0 / sqrt(dot3(r0, r1, r2, r0, r1, r2));
+    d[0] = r0 * inv; d[1] = r1 * inv; d[2] = r2 * inv;
 }
 
 // Trace modes, all running the same bounce loop (src/raytracer.ts:168-277):
@@ -721,8 +751,10 @@ enum { TR_FUSED = 0, TR_LIST = 1 };
 template <bool STATS, int MODE>
 __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg, bool cull,
                           int diag, const double cam_pos[3], const double dir0[3], RayResult &R, Counters &c,
-                          int cn, const ListHit &pre, const RtCont *rs, const RayQueues &Q, int pix)
+                          int cn, const ListHit &pre, const RtCont *rs, const RayQueues &Q, int pix,
+                          const RtLaunch &L)
 {
+    uint32_t draws = rs ? (uint32_t)rs->pad[1] : 0u;   // RT_SCATTER_COUNTER draws used by this ray
     constexpr bool LIST = MODE == TR_LIST;
     double o[3], d[3];
     double col0, col1, col2, path;
@@ -819,7 +851,10 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
             if (!sh.mirror) goto done;                          // matte: terminal
             const double k2 = -dot3(d[0], d[1], d[2], h.n[0], h.n[1], h.n[2]) * 2;   // vector.reflection
             d[0] = d[0] + h.n[0] * k2; d[1] = d[1] + h.n[1] * k2; d[2] = d[2] + h.n[2] * k2;
-            if (sh.roughness > 0.0) { R.status = ST_FAULT; goto done; }  // excluded by the host check
+            if (sh.roughness > 0.0) {                                                  // :233-235
+                if (cfg.scatter_mode != RT_SCATTER_COUNTER) { R.status = ST_FAULT; goto done; }
+                scatter_dir(cfg.scatter_seed, frame_pixel(L, pix), draws, h.n, sh.roughness, d);
+            }
             o[0] += d[0] * 1e-3; o[1] += d[1] * 1e-3; o[2] += d[2] * 1e-3;   // move_slightly_forward
         } else if (sh.response == RT_RESP_TRANSMISSION) {
             o[0] += d[0] * 1e-3; o[1] += d[1] * 1e-3; o[2] += d[2] * 1e-3;
@@ -857,7 +892,7 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
                 goto done;
             }
             queue_push(Q.last ? Q.ovf : Q.next, Q.last ? Q.ovf_n : Q.next_n, o, d, col0, col1, col2, path, refcount,
-                       cur_sub, R, pix, 0);
+                       cur_sub, R, pix, 0, draws);
             R.status = ST_DEFER;
             return;
         }
@@ -977,7 +1012,7 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
             R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.segments = 1; R.status = ST_FAULT;
         } else {
             trace_ray<STATS, TR_FUSED>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, -1, none,
-                                       nullptr, Q, src.pix);
+                                       nullptr, Q, src.pix, L);
         }
         write_pixel(L, src.id, R);
         if (STATS) {
@@ -1119,14 +1154,14 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
                 L.ovf[k] = *src.rec;
             } else {
                 R.hit_ent = -1; R.hit_node = -1; R.segments = 1;
-                queue_push(L.ovf, L.ctr, src.o, src.d, 1, 1, 1, 0, 0, F.start_sub, R, src.pix, 1);
+                queue_push(L.ovf, L.ctr, src.o, src.d, 1, 1, 1, 0, 0, F.start_sub, R, src.pix, 1, 0u);
             }
             continue;
         }
         const int2 fh = reinterpret_cast<const int2 *>(L.first)[src.id];
         const ListHit pre = {fh.x, fh.y, fh.y >= 0 ? L.scene.prim[fh.y].rank : 0};
         trace_ray<false, TR_LIST>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, cn, pre, src.rec, Q,
-                                  src.pix);
+                                  src.pix, L);
         if (R.status == ST_DEFER) continue;
         write_pixel(L, (size_t)src.pix, R);
     }
@@ -1151,7 +1186,7 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
         const RtCont *e = L.ovf + q;
         RayResult R;
         trace_ray<false, TR_FUSED>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, e->d, R, c, -1, none, e, Q,
-                                   e->pix);
+                                   e->pix, L);
         write_pixel(L, (size_t)e->pix, R);
     }
 }

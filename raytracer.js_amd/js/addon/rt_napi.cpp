@@ -95,6 +95,18 @@ bool get_number(napi_env env, napi_value obj, const char *key, double &out)
     return true;
 }
 
+// optional numeric property: `out` keeps its value when the property is absent / undefined
+bool get_number_opt(napi_env env, napi_value obj, const char *key, double &out)
+{
+    bool has = false;
+    if (napi_has_named_property(env, obj, key, &has) != napi_ok || !has) return true;
+    napi_value v;
+    napi_valuetype vt;
+    if (napi_get_named_property(env, obj, key, &v) != napi_ok || napi_typeof(env, v, &vt) != napi_ok) return false;
+    if (vt == napi_undefined) return true;
+    return get_number(env, obj, key, out);
+}
+
 bool get_vec(napi_env env, napi_value obj, const char *key, double *out, uint32_t n)
 {
     napi_value v;
@@ -265,6 +277,11 @@ napi_value TraceFrame(napi_env env, napi_callback_info info)
     cfg.default_substance = (int32_t)defsub;
     cfg.distance_attenuation_factor = att;
     cfg.col_weight = wgt;
+    double seed = 0, smode = RT_SCATTER_REJECT;
+    if (!get_number_opt(env, argv[2], "scatter_seed", seed) || !get_number_opt(env, argv[2], "scatter_mode", smode))
+        return nullptr;
+    cfg.scatter_seed = seed > 0 ? (uint64_t)seed : 0;
+    cfg.scatter_mode = (int32_t)smode;
     auto typed_arg = [&](size_t i, napi_typedarray_type want, Typed &t) -> bool {
         if (argc <= i) return false;
         napi_valuetype vt;

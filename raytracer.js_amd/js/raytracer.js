@@ -204,7 +204,10 @@ function camera_desc(camera) {
 /* ---- the drop-in ------------------------------------------------------------------------------- */
 
 class Raytracer {
-	/** Same signature as the reference (src/raytracer.ts:291-298); `options.device` picks the GPU. */
+	/** Same signature as the reference (src/raytracer.ts:291-298); `options.device` picks the GPU.
+	 * `options.scatter === 'counter'` renders rough mirrors with the counter-based RNG (include/rt.h
+	 * RT_SCATTER_COUNTER), keyed each frame by one draw of this Raytracer's rng; otherwise they are
+	 * rejected (RT_E_UNSUPPORTED), as scatter_ray's sequential PRNG cannot be reproduced in parallel. */
 	constructor(config, otree, camera, ebuffer, rng, options) {
 		this.camera = camera;
 		this.ebuffer = ebuffer;
@@ -259,6 +262,10 @@ class Raytracer {
 			distance_attenuation_factor: this.config.distance_attenuation_factor,
 			col_weight: eb.col_weight
 		};
+		if (this.options.scatter === 'counter') {
+			cfg.scatter_mode = 1;
+			cfg.scatter_seed = Math.floor(this._rng.next() * 9007199254740992);   // one draw per frame
+		}
 		const P = cam.width * cam.height;
 		if (this.options.keep_ids) {
 			if (!this.last_hit_entity || this.last_hit_entity.length !== P) {

@@ -55,7 +55,11 @@ class rt_camera_desc(C.Structure):
 
 class rt_config_desc(C.Structure):
     _fields_ = [("refmax", _i), ("default_substance", _i), ("sky_rgb", _d * 3),
-                ("distance_attenuation_factor", _d), ("col_weight", _d)]
+                ("distance_attenuation_factor", _d), ("col_weight", _d), ("scatter_seed", C.c_uint64),
+                ("scatter_mode", _i), ("pad_", _i)]
+
+
+RT_SCATTER_REJECT, RT_SCATTER_COUNTER = 0, 1
 
 
 class rt_stats(C.Structure):

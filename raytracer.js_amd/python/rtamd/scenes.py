@@ -130,6 +130,16 @@ def config1_spheres():
     return SceneSpec("config1_8spheres", ents, shades)
 
 
+def roughen(spec, values=(0.05, 0.3, 0.8)):
+    """Copy of `spec` with roughness_index > 0 on every mirror shade, cycling through `values`
+    (rough mirrors: Ray.scatter_ray, src/raytracer.ts:121-133,233-235)."""
+    sh = spec.shades.copy()
+    idx = np.nonzero(sh["mirror"])[0]
+    for k, i in enumerate(idx):
+        sh["roughness"][i] = values[k % len(values)]
+    return SceneSpec(spec.name + "_rough", spec.entities, sh, spec.substances, spec.root_pos, spec.root_size)
+
+
 def random_triangles(st, n, half_extent, lo=0.02, hi=0.98, max_in_depth=6):
     c = lo + (hi - lo) * st.take(n * 3).reshape(n, 3)
     off = (st.take(n * 9).reshape(n, 3, 3) * 2 - 1) * half_extent
@@ -240,13 +250,16 @@ def make_camera(width, height, pos=(0.5, 0.5, 0.5), init_v=0.0, init_h=math.pi /
     return cam
 
 
-def make_config(refmax, sky=SKY_RGB, atten=1.0, default_substance=SUB_AIR, col_weight=1.0):
+def make_config(refmax, sky=SKY_RGB, atten=1.0, default_substance=SUB_AIR, col_weight=1.0, scatter_seed=None):
+    """scatter_seed: None = RT_SCATTER_REJECT (rough mirrors unsupported), else RT_SCATTER_COUNTER."""
     c = abi.rt_config_desc()
     c.refmax = int(refmax)
     c.default_substance = int(default_substance)
     c.sky_rgb[:] = [float(x) for x in sky]
     c.distance_attenuation_factor = float(atten)
     c.col_weight = float(col_weight)
+    c.scatter_mode = abi.RT_SCATTER_REJECT if scatter_seed is None else abi.RT_SCATTER_COUNTER
+    c.scatter_seed = 0 if scatter_seed is None else int(scatter_seed) & (2 ** 64 - 1)
     return c
 
 

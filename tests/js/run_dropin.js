@@ -1,7 +1,8 @@
 /*
- * run_dropin.js <scene.json> <out_prefix> [--serialize-only]
+ * run_dropin.js <scene.json> <out_prefix> [--serialize-only] [--scatter <seed>]
  * Builds reference-shaped objects, checks serialize_scene() reproduces the linearised arrays, and
  * (unless --serialize-only) renders one frame with the drop-in Raytracer into ExposureBuffer.pixels.
+ * --scatter: rough mirrors with options.scatter = 'counter', the rng's one draw = seed / 2^53.
  */
 'use strict';
 const fs = require('fs');
@@ -43,7 +44,11 @@ const config = {
 	refmax: sc.cfg.refmax, default_substance: def_sub, distance_attenuation_factor: sc.cfg.atten,
 	sky: { texture: new rs.SolidTexture({ r: sc.cfg.sky[0], g: sc.cfg.sky[1], b: sc.cfg.sky[2], a: 1 }) }
 };
-const tracer = new rt.Raytracer(config, world.root, cam, eb, null, { keep_ids: true });
+const si = process.argv.indexOf('--scatter');
+const seed = si > 0 ? Number(process.argv[si + 1]) : null;
+const rng = seed === null ? null : { next: () => seed / 9007199254740992 };
+const tracer = new rt.Raytracer(config, world.root, cam, eb, rng,
+	seed === null ? { keep_ids: true } : { keep_ids: true, scatter: 'counter' });
 const t0 = process.hrtime.bigint();
 tracer.trace_frame();
 const t1 = process.hrtime.bigint();

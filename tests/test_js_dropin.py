@@ -57,19 +57,23 @@ def test_serialize_matches_native_builder(tmp_path, name):
 def test_addon_loads_and_fails_loudly_without_gpu():
     """The addon loads; with no GPU create() throws RT_E_NODEVICE (never a silent CPU path)."""
     js = ("const rt=require(%r);const a=rt.load_addon();"
-          "if(a.abiVersion()!==1)throw Error('abi');"
+          "if(a.abiVersion()!==2)throw Error('abi');"
           "try{a.create(0);console.log('GPU')}catch(e){console.log(e.code)}") % os.path.join(ROOT, "raytracer.js_amd", "js", "raytracer.js")
     out = _node(["-e", js]).strip()
     assert out in ("GPU", "RT_E_NODEVICE")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,wh,refmax", [("config1", (256, 256), 2), ("small4", (200, 150), 3)])
+@pytest.mark.parametrize("name,wh,refmax", [("config1", (256, 256), 2), ("small4", (200, 150), 3),
+                                            ("small4_rough", (200, 150), 4)])
 def test_dropin_frame_equals_oracle(tmp_path, name, wh, refmax):
-    spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4)}[name]()
-    cam, cfg = scenes.make_camera(*wh), scenes.make_config(refmax)
+    """small4_rough: rough mirrors through options.scatter = 'counter' (RT_SCATTER_COUNTER)."""
+    spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4),
+            "small4_rough": lambda: scenes.roughen(scenes.small_random(4, p_mirror=0.5))}[name]()
+    seed = 123456789012345 if name.endswith("rough") else None
+    cam, cfg = scenes.make_camera(*wh), scenes.make_config(refmax, scatter_seed=seed)
     path = _dump(tmp_path, spec, cam, cfg)
-    _node([RUNNER, path, str(tmp_path / "out")])
+    _node([RUNNER, path, str(tmp_path / "out")] + (["--scatter", str(seed)] if seed else []))
     P = wh[0] * wh[1]
     rgb = np.fromfile(tmp_path / "out.rgb", dtype=np.float32)
     ent = np.fromfile(tmp_path / "out.ent", dtype=np.int32)
