@@ -9,6 +9,8 @@
  *   rt_upload_scene  <- the EntityOtree the Raytracer holds (src/octree_entity.ts:27, src/octree.ts:25-126)
  *                       flattened: nodes in DFS pre-order (children 0..7), per-node entity lists in
  *                       EntitySet (insertion) order (src/octree_entity.ts:32-49, src/entity.ts:50-56)
+ *   rt_update_scene  <- the same tree after add_entity_to_octree / Entity.set_octree / set_material
+ *                       edits (src/octree_entity.ts:174-188, src/entity.ts:50-56): incremental
  *   rt_trace_frame   <- Raytracer.trace_frame()  src/raytracer.ts:308-330  (camera scan
  *                       src/view/camera.ts:207-250, Ray.trace src/raytracer.ts:168-277,
  *                       ExposureBuffer.set_color src/view/exposure_buffer.ts:68-91)
@@ -182,6 +184,30 @@ int  rt_abi_version(void);
 /* Copies the scene to device memory (the caller keeps ownership of every array). */
 int  rt_upload_scene(rt_ctx *ctx, const rt_scene_desc *scene);
 
+/* Incremental re-upload after the host edited the scene:
+ * entities added with add_entity_to_octree (src/octree_entity.ts:174-188), moved (Entity._set_pos
+ * + add_entity_to_octree, which re-files them with Entity.set_octree, src/entity.ts:50-56), or
+ * given another material / texture / substance.  `scene` is the complete new scene, with the same
+ * contract as rt_upload_scene, plus: entity ids are stable (an existing entity keeps its index,
+ * new ones are appended) and the root cube is unchanged.  The resident scene is diffed against it
+ * and only what changed is rebuilt and sent: the cull hierarchies of nodes whose entity list or
+ * member geometry changed, new nodes, and the changed table entries, in one staging copy and one
+ * scatter kernel.  Results are identical to rt_upload_scene of the same scene.  Falls back to a
+ * full (compacting) upload when the scene is not an edit of the resident one or most of it
+ * changed.  Synchronises the device first: no frame may be in flight on another stream. */
+typedef struct rt_update_stats {
+    int32_t full;             /* 1: this call did a full upload                           */
+    int32_t dirty_nodes;      /* nodes whose entity list / cull hierarchy was rebuilt     */
+    int32_t new_nodes;        /* octree nodes created since the resident scene            */
+    int32_t moved_regions;    /* dirty nodes that outgrew their pool region               */
+    int32_t changed_entities; /* entities whose geometry / shade / substance changed      */
+    int32_t pad_;
+    int64_t bytes;            /* host-to-device bytes sent by this call                   */
+    double  host_ms;          /* diff + rebuild on the host                               */
+    double  total_ms;         /* the whole call, including the copy and the patch kernel  */
+} rt_update_stats;
+int  rt_update_scene(rt_ctx *ctx, const rt_scene_desc *scene, rt_update_stats *stats);
+
 /* Full frame, host buffers.  rgb_inout is the ExposureBuffer's Float32Array (W*H*3, row-major,
  * interleaved RGB); it is read (when col_weight != 1) and written.  hit_entity / hit_node
  * (W*H int32, nullable) receive the entity id / DFS node id of the primary collision, -1 for none.
@@ -261,6 +287,14 @@ void rt_builder_destroy(rt_builder *b);
 /* add_entity_to_octree(root, entity, {max_in_depth, max_out_depth}); *entity_id = creation index */
 int  rt_builder_add(rt_builder *b, const rt_entity_in *e, int32_t *entity_id);
 int  rt_builder_add_many(rt_builder *b, const rt_entity_in *e, int32_t n);
+/* Entity._set_pos(pos) then add_entity_to_octree(root, entity, its original flags): the entity
+ * leaves its EntitySet and is appended to the covering node's set, even when that is the same
+ * node (Set.delete + Set.add, src/entity.ts:50-56).  pos: SPHERE centre (the sphere_math caches
+ * follow, src/math/intersection.ts:94-97), BOX min corner, FACE centroid (the triangle is
+ * translated; raytracer.js_amd/js FaceEntity._set_pos). */
+int  rt_builder_move(rt_builder *b, int32_t entity_id, const double pos[3]);
+/* Entity.set_material / set_texture / set_substance: the entity's shade and substance indices. */
+int  rt_builder_set_shade(rt_builder *b, int32_t entity_id, int32_t shade, int32_t substance);
 /* Linearise (DFS pre-order) into `out`; shade/substance tables are passed through.  Pointers in
  * `out` stay valid until the next rt_builder_* call on `b`. */
 int  rt_builder_desc(rt_builder *b, const rt_shade *shades, int32_t n_shades,

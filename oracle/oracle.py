@@ -63,6 +63,8 @@ def lib():
     L.orc_tonemap_range.argtypes = [i, pd, i, C.c_double, C.c_double, pd]
     L.orc_tonemap.argtypes = [pf, C.c_int64, C.c_double, C.c_double, C.POINTER(C.c_uint8)]
     L.orc_tonemap.restype = None
+    L.orc_move_entity.argtypes = [vp, vp, i, pd, i, i]
+    L.orc_set_shade.argtypes = [vp, i, i, i]
     L.orc_counter_draw_at.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
     L.orc_counter_draw_at.restype = C.c_double
     L.orc_scatter_dir.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, pd, C.c_double, pd]
@@ -179,6 +181,16 @@ class World:
         for e in ents:
             self.add_entity(tree, e["type"], e["geom"], e["shade"], e["substance"],
                             e["max_in_depth"], e["max_out_depth"])
+
+    def move_entity(self, tree, eid, pos, max_in_depth=10, max_out_depth=0):
+        """Entity._set_pos(pos) + add_entity_to_octree: re-filed at the end of its new node's Set."""
+        r = self.L.orc_move_entity(self.h, tree, int(eid), _vec(pos), int(max_in_depth), int(max_out_depth))
+        if r < 0:
+            raise RuntimeError("move (add_entity_to_octree) threw (%d)" % r)
+
+    def set_shade(self, eid, shade, substance):
+        if self.L.orc_set_shade(self.h, int(eid), int(shade), int(substance)) < 0:
+            raise RuntimeError("bad entity %r" % eid)
 
     def in_set(self, tree, eid):
         return bool(self.L.orc_entity_in_set(tree, int(eid)))

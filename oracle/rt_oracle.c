@@ -688,6 +688,55 @@ int orc_add_entity(oworld *w, onode *tree, int type, const double geom[9], int s
     return id;
 }
 
+/* Entity._set_pos(pos) then add_entity_to_octree(tree, entity, flags) — the edit a host makes to
+ * move an entity.  _set_pos: SphereEntity (src/entities/entity_sphere.ts:55-61; sphere_math.pos
+ * runs Sphere.update_cache, src/math/intersection.ts:94-97, recomputing _dot_pp and, to the same
+ * value, _radius_sq), BasicEntity (src/entities/entity_basic.ts:38-42), the build's FaceEntity
+ * (translate so the centroid lands on pos).  Then Entity.set_octree (src/entity.ts:50-56):
+ * Set.delete from the old node, Set.add to the fitting one — to the END of its Set order, even
+ * when it is the same node. */
+int orc_move_entity(oworld *w, onode *tree, int id, const double pos[3], int max_in_depth, int max_out_depth)
+{
+    if (id < 0 || id >= w->n_ents) return RT_E_INVALID;
+    oentity *e = &w->ents[id];
+    if (e->type == RT_ENT_SPHERE) {
+        for (int i = 0; i < 3; i++) e->g[i] = pos[i];
+        e->g[4] = vdot(pos, pos);
+    } else if (e->type == RT_ENT_BOX) {
+        for (int i = 0; i < 3; i++) e->g[i] = pos[i];
+    } else {
+        double d[3];
+        for (int i = 0; i < 3; i++) d[i] = pos[i] - (e->g[i] + e->g[3 + i] + e->g[6 + i]) / 3;
+        for (int v = 0; v < 3; v++)
+            for (int i = 0; i < 3; i++) e->g[3 * v + i] += d[i];
+    }
+    double apos[3], asize;
+    entity_aabb(e, apos, &asize);
+    onode *fit = NULL;
+    if (covering_node(tree, apos, asize, &fit) < 0) return RT_E_TREE;
+    if (fit == NULL) {
+        onode *abs_root = get_root(tree);
+        fit = extend_outside(w, tree, abs_root, apos, asize, max_out_depth);
+        if (!fit) return RT_E_TREE;
+    }
+    fit = extend_inside(w, tree, fit, apos, asize, max_in_depth);
+    if (!fit) return RT_E_TREE;
+    e = &w->ents[id];
+    if (e->octree != NULL) set_delete(e->octree, id);
+    e->octree = fit;
+    set_add(fit, id);
+    return 0;
+}
+
+/* Entity.set_material / set_texture / set_substance */
+int orc_set_shade(oworld *w, int id, int shade, int substance)
+{
+    if (id < 0 || id >= w->n_ents) return RT_E_INVALID;
+    w->ents[id].shade = shade;
+    w->ents[id].substance = substance;
+    return 0;
+}
+
 /* is_within: sphere src/entities/entity_sphere.ts:63-66, box src/entities/entity_box.ts:47-52
  * (pos as MIN corner), face: false. */
 static int entity_is_within(const oentity *e, const double p[3])

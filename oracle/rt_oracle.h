@@ -61,6 +61,9 @@ int  orc_set_tables(oworld *w, const rt_shade *shades, int n_shades, const doubl
  * (creation order) or <0; *fitting receives the node holding the entity. */
 int  orc_add_entity(oworld *w, onode *tree, int type, const double geom[9], int shade, int substance,
                     int max_in_depth, int max_out_depth, onode **fitting);
+/* Entity._set_pos + add_entity_to_octree (re-filed at the end of the fitting node's Set order) */
+int  orc_move_entity(oworld *w, onode *tree, int entity_id, const double pos[3], int max_in_depth, int max_out_depth);
+int  orc_set_shade(oworld *w, int entity_id, int shade, int substance);
 int  orc_entity_in_set(onode *t, int entity_id);                          /* EntitySet.set.has */
 int  orc_entity_at_pos(oworld *w, onode *tree, const double p[3]);       /* :191-202, -1 = undefined */
 

@@ -65,9 +65,6 @@ struct DevBuf {
 
 }  // namespace
 
-int rt_build_cull(const rt_scene_desc *s, std::vector<RtPrim> &prim, std::vector<RtBvh> &bvh,
-                  std::vector<int32_t> &node_ent, std::vector<int32_t> &prefix, bool sah);
-
 struct rt_ctx {
     int device = 0;
     int flags = 0;
@@ -82,8 +79,7 @@ struct rt_ctx {
     bool has_scene = false;
     bool scatter = false;            // a mirror shade with roughness > 0 is reachable
     RtDevScene scene{};
-    DevBuf b_node_ps, b_node_child, b_node_up, b_node_ent, b_prim, b_shades, b_ent_sub, b_sub_ri;
-    DevBuf b_bvh, b_list, b_prefix;
+    RtSceneStore *store = nullptr;   // the resident scene (rt_scene.hip)
     DevBuf b_stat, b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_fr, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
     DevBuf b_walk;
     static constexpr int NEV = 256;
@@ -124,6 +120,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     for (int i = 0; r == RT_OK && i < rt_ctx::NEV; i++)
         if (hipEventCreate(&c->ev[i][0]) != hipSuccess || hipEventCreate(&c->ev[i][1]) != hipSuccess)
             r = rt_set_error(RT_E_HIP, "rt_create: hipEventCreate failed");
+    if (r == RT_OK && !(c->store = rt_store_new(c->bvh_sah))) r = rt_set_error(RT_E_INVALID, "rt_create: out of memory");
     if (r == RT_OK) r = c->b_setup.ensure(sizeof(RtFrameSetup));
     if (r == RT_OK) r = c->b_counters.ensure(sizeof(unsigned long long) * CT_N);
     if (r == RT_OK) r = c->b_fault.ensure(sizeof(int));   // ray fault flag
@@ -141,10 +138,11 @@ extern "C" void rt_destroy(rt_ctx *c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    DevBuf *bufs[] = {&c->b_node_ps, &c->b_node_child, &c->b_node_up, &c->b_node_ent, &c->b_prim,
-                      &c->b_shades, &c->b_ent_sub, &c->b_sub_ri, &c->b_stat, &c->b_cand, &c->b_cand_n, &c->b_first, &c->b_queue, &c->b_ctr, &c->b_setup, &c->b_fr, &c->b_dirs,
+    rt_store_free(c->store);
+    c->store = nullptr;
+    DevBuf *bufs[] = {&c->b_stat, &c->b_cand, &c->b_cand_n, &c->b_first, &c->b_queue, &c->b_ctr, &c->b_setup, &c->b_fr, &c->b_dirs,
                       &c->b_rgb, &c->b_hit_e, &c->b_hit_n, &c->b_status, &c->b_counters, &c->b_fault,
-                      &c->b_walk, &c->b_bvh, &c->b_list, &c->b_prefix};
+                      &c->b_walk};
     for (DevBuf *b : bufs) b->release();
     for (int i = 0; i < rt_ctx::NEV; i++)
         for (int k = 0; k < 2; k++)
@@ -153,131 +151,24 @@ extern "C" void rt_destroy(rt_ctx *c)
     delete c;
 }
 
-template <typename T>
-static int upload(rt_ctx *c, DevBuf &b, const T *src, size_t n)
-{
-    int r = b.ensure(sizeof(T) * (n ? n : 1));
-    if (r != RT_OK) return r;
-    if (n) HIP_TRY(hipMemcpyAsync(b.p, src, sizeof(T) * n, hipMemcpyHostToDevice, c->stream));
-    return RT_OK;
-}
-
 extern "C" int rt_upload_scene(rt_ctx *c, const rt_scene_desc *s)
 {
     if (!c || !s) return rt_set_error(RT_E_INVALID, "rt_upload_scene: null argument");
-    const int N = s->n_nodes, NL = s->n_list, NE = s->n_entities;
-    if (N < 1 || NL < 0 || NE < 0 || s->n_shades < 0 || s->n_substances < 0)
-        return rt_set_error(RT_E_INVALID, "rt_upload_scene: bad counts");
-    if (!s->node_pos || !s->node_size || !s->node_parent || !s->node_child || !s->node_ent_begin ||
-        !s->node_ent_count || (NL && !s->list_entity) || (NE && (!s->ent_type || !s->ent_geom || !s->ent_shade || !s->ent_substance)) ||
-        (s->n_shades && !s->shades) || (s->n_substances && !s->substance_ri))
-        return rt_set_error(RT_E_INVALID, "rt_upload_scene: null array");
-    if (s->node_parent[0] != -1) return rt_set_error(RT_E_INVALID, "rt_upload_scene: node 0 must be the root");
-
-    std::vector<double> ps(4 * (size_t)N);
-    std::vector<int32_t> up(2 * (size_t)N), ent(2 * (size_t)N);
-    for (int n = 0; n < N; n++) {
-        for (int i = 0; i < 3; i++) ps[4 * n + i] = s->node_pos[3 * n + i];
-        ps[4 * n + 3] = s->node_size[n];
-        const int p = s->node_parent[n];
-        if (n > 0 && (p < 0 || p >= N)) return rt_set_error(RT_E_INVALID, "rt_upload_scene: node %d parent %d", n, p);
-        for (int k = 0; k < 8; k++) {
-            const int ch = s->node_child[8 * n + k];
-            if (ch < -1 || ch >= N || ch == 0) return rt_set_error(RT_E_INVALID, "rt_upload_scene: node %d child %d", n, ch);
-            if (ch > 0 && s->node_parent[ch] != n)
-                return rt_set_error(RT_E_INVALID, "rt_upload_scene: child %d of %d has parent %d", ch, n, s->node_parent[ch]);
-        }
-        up[2 * n] = n == 0 ? -1 : p;
-        if (n == 0) {
-            up[2 * n + 1] = RT_OCT_UNDEF;
-        } else {
-            // index_within_parent (src/octree_space.ts:113-125): geometric, never cached
-            const double sc = 2 / s->node_size[p];
-            const int32_t ix = rtjs::toint32((s->node_pos[3 * n + 0] - s->node_pos[3 * p + 0]) * sc);
-            const int32_t iy = rtjs::toint32((s->node_pos[3 * n + 1] - s->node_pos[3 * p + 1]) * sc);
-            const int32_t iz = rtjs::toint32((s->node_pos[3 * n + 2] - s->node_pos[3 * p + 2]) * sc);
-            const double idx = rtjs::octant_sum(ix, iy, iz);
-            up[2 * n + 1] = (idx >= 0 && idx <= 7) ? (int)idx : RT_OCT_BAD;
-        }
-        const int b = s->node_ent_begin[n], cnt = s->node_ent_count[n];
-        if (b < 0 || cnt < 0 || (long long)b + cnt > NL)
-            return rt_set_error(RT_E_INVALID, "rt_upload_scene: node %d entity range", n);
-        ent[2 * n] = b;
-        ent[2 * n + 1] = cnt;
-    }
-    for (int e = 0; e < NE; e++) {
-        if (s->ent_type[e] < RT_ENT_SPHERE || s->ent_type[e] > RT_ENT_FACE)
-            return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d type", e);
-        if (s->ent_shade[e] < 0 || s->ent_shade[e] >= s->n_shades)
-            return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d shade", e);
-        if (s->ent_substance[e] < -1 || s->ent_substance[e] >= s->n_substances)
-            return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d substance", e);
-    }
-    bool scatter = false;
-    std::vector<RtPrim> prim((size_t)(NL ? NL : 1));
-    for (int k = 0; k < NL; k++) {
-        const int e = s->list_entity[k];
-        if (e < 0 || e >= NE) return rt_set_error(RT_E_INVALID, "rt_upload_scene: list entry %d entity %d", k, e);
-        const double *g = s->ent_geom + 9 * (size_t)e;
-        RtPrim &p = prim[k];
-        memset(&p, 0, sizeof p);
-        const int type = s->ent_type[e];
-        if (type == RT_ENT_SPHERE) {
-            p.g[0] = g[0]; p.g[1] = g[1]; p.g[2] = g[2];
-            p.g[3] = g[4];            // _dot_pp
-            p.g[4] = g[5];            // Sphere._radius_sq
-            p.g[5] = g[6];            // SphereEntity._radius_sq (is_within)
-            p.g[6] = 2 / g[3];        // 2 / diameter (normal scale)
-        } else if (type == RT_ENT_BOX) {
-            p.g[0] = g[0]; p.g[1] = g[1]; p.g[2] = g[2]; p.g[3] = g[3];
-        } else {
-            for (int i = 0; i < 3; i++) {
-                p.g[i] = g[i];
-                p.g[3 + i] = g[3 + i] - g[i];   // e1 = v1 - v0
-                p.g[6 + i] = g[6 + i] - g[i];   // e2 = v2 - v0
-            }
-        }
-        p.meta = type | (s->ent_shade[e] << 2);
-        p.rank = k;
-        const rt_shade &sh = s->shades[s->ent_shade[e]];
-        if (!sh.light && sh.response == RT_RESP_REFLECTION && sh.mirror && sh.roughness > 0.0) scatter = true;
-    }
-    (void)ent;
-    // per-node cull hierarchies; prims are re-ordered within each node's range
-    std::vector<RtBvh> bvh;
-    std::vector<int32_t> ent4, prefix;
-    if (NL == 0) prim.clear();
-    int r = rt_build_cull(s, prim, bvh, ent4, prefix, c->bvh_sah);
+    int r = use_device(c);
     if (r != RT_OK) return r;
-    if ((r = use_device(c)) != RT_OK) return r;
     c->has_scene = false;
-    if ((r = upload(c, c->b_node_ps, ps.data(), ps.size())) != RT_OK) return r;
-    if ((r = upload(c, c->b_node_child, s->node_child, 8 * (size_t)N)) != RT_OK) return r;
-    if ((r = upload(c, c->b_node_up, up.data(), up.size())) != RT_OK) return r;
-    if ((r = upload(c, c->b_node_ent, ent4.data(), ent4.size())) != RT_OK) return r;
-    if ((r = upload(c, c->b_prim, prim.data(), prim.size())) != RT_OK) return r;
-    if ((r = upload(c, c->b_bvh, bvh.data(), bvh.size())) != RT_OK) return r;
-    if ((r = upload(c, c->b_list, s->list_entity, (size_t)NL)) != RT_OK) return r;
-    if ((r = upload(c, c->b_prefix, prefix.data(), prefix.size())) != RT_OK) return r;
-    if ((r = upload(c, c->b_shades, s->shades, (size_t)s->n_shades)) != RT_OK) return r;
-    if ((r = upload(c, c->b_ent_sub, s->ent_substance, (size_t)NE)) != RT_OK) return r;
-    if ((r = upload(c, c->b_sub_ri, s->substance_ri, (size_t)s->n_substances)) != RT_OK) return r;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    RtDevScene &d = c->scene;
-    d.node_ps = (const double *)c->b_node_ps.p;
-    d.node_child = (const int32_t *)c->b_node_child.p;
-    d.node_up = (const int32_t *)c->b_node_up.p;
-    d.node_ent = (const int32_t *)c->b_node_ent.p;
-    d.prim = (const RtPrim *)c->b_prim.p;
-    d.bvh = (const RtBvh *)c->b_bvh.p;
-    d.list_entity = (const int32_t *)c->b_list.p;
-    d.list_prefix = (const int32_t *)c->b_prefix.p;
-    d.shades = (const rt_shade *)c->b_shades.p;
-    d.ent_sub = (const int32_t *)c->b_ent_sub.p;
-    d.sub_ri = (const double *)c->b_sub_ri.p;
-    d.n_nodes = N; d.n_list = NL; d.n_entities = NE; d.n_shades = s->n_shades; d.n_subs = s->n_substances;
-    d.n_bvh = (int32_t)bvh.size();
-    c->scatter = scatter;
+    if ((r = rt_store_upload(c->store, s, false, c->stream, &c->scene, &c->scatter, nullptr)) != RT_OK) return r;
+    c->has_scene = true;
+    return RT_OK;
+}
+
+extern "C" int rt_update_scene(rt_ctx *c, const rt_scene_desc *s, rt_update_stats *stats)
+{
+    if (!c || !s) return rt_set_error(RT_E_INVALID, "rt_update_scene: null argument");
+    int r = use_device(c);
+    if (r != RT_OK) return r;
+    c->has_scene = false;
+    if ((r = rt_store_upload(c->store, s, true, c->stream, &c->scene, &c->scatter, stats)) != RT_OK) return r;
     c->has_scene = true;
     return RT_OK;
 }

@@ -32,6 +32,7 @@ struct BEnt {
     int type;
     double g[9];
     int shade, substance;
+    int max_in, max_out;    // AddEntityToOctreeFlags it was added with (reused by rt_builder_move)
     int owner;              // Entity._octree (-1 = none)
 };
 
@@ -195,6 +196,33 @@ static int extend_outside(rt_builder *b, int root, int node, const double a[3], 
     return -1;
 }
 
+// get_covering_node_for_entity + extend_tree_outside/inside (src/octree_entity.ts:60-188): the
+// node add_entity_to_octree files `e` under (may grow the tree).
+static int place(rt_builder *b, const BEnt &e, int *fit_out)
+{
+    double a[3], asize;
+    entity_aabb(e, a, &asize);
+    int fit = -1, deepest;
+    int r = node_at_pos(b, b->root, a, &deepest);
+    if (r < 0) return rt_set_error(RT_E_TREE, "add_entity_to_octree: Node index out of range (0..7)");
+    if (r == 1) {
+        int cur = deepest;
+        do {
+            if (aabb_in_cube(a, asize, b->nodes[cur].pos, b->nodes[cur].size)) break;
+            cur = b->nodes[cur].parent;
+        } while (cur >= 0);
+        fit = cur;
+    }
+    if (fit < 0) {
+        fit = extend_outside(b, b->root, get_root(b, b->root), a, asize, e.max_out);
+        if (fit < 0) return rt_set_error(RT_E_TREE, "TreeOutsideGrowError: The tree outside-depth limit exceeded");
+    }
+    fit = extend_inside(b, b->root, fit, a, asize, e.max_in);
+    if (fit < 0) return rt_set_error(RT_E_TREE, "add_entity_to_octree: Node index out of range (0..7)");
+    *fit_out = fit;
+    return RT_OK;
+}
+
 extern "C" int rt_builder_create(const double root_pos[3], double root_size, rt_builder **out)
 {
     if (!root_pos || !out) return rt_set_error(RT_E_INVALID, "rt_builder_create: null argument");
@@ -230,31 +258,60 @@ extern "C" int rt_builder_add(rt_builder *b, const rt_entity_in *in, int32_t *en
     e.substance = in->substance;
     e.owner = -1;
 
-    double a[3], asize;
-    entity_aabb(e, a, &asize);
-    // get_covering_node_for_entity
-    int fit = -1, deepest;
-    int r = node_at_pos(b, b->root, a, &deepest);
-    if (r < 0) return rt_set_error(RT_E_TREE, "add_entity_to_octree: Node index out of range (0..7)");
-    if (r == 1) {
-        int cur = deepest;
-        do {
-            if (aabb_in_cube(a, asize, b->nodes[cur].pos, b->nodes[cur].size)) break;
-            cur = b->nodes[cur].parent;
-        } while (cur >= 0);
-        fit = cur;
-    }
-    if (fit < 0) {
-        fit = extend_outside(b, b->root, get_root(b, b->root), a, asize, in->max_out_depth);
-        if (fit < 0) return rt_set_error(RT_E_TREE, "TreeOutsideGrowError: The tree outside-depth limit exceeded");
-    }
-    fit = extend_inside(b, b->root, fit, a, asize, in->max_in_depth);
-    if (fit < 0) return rt_set_error(RT_E_TREE, "add_entity_to_octree: Node index out of range (0..7)");
+    e.max_in = in->max_in_depth;
+    e.max_out = in->max_out_depth;
+    int fit;
+    int r = place(b, e, &fit);
+    if (r != RT_OK) return r;
     int id = (int)b->ents.size();
     e.owner = fit;
     b->ents.push_back(e);
     b->nodes[fit].set.push_back(id);   // a fresh entity: Set.add appends
     if (entity_id) *entity_id = id;
+    return RT_OK;
+}
+
+extern "C" int rt_builder_move(rt_builder *b, int32_t id, const double pos[3])
+{
+    if (!b || !pos) return rt_set_error(RT_E_INVALID, "rt_builder_move: null argument");
+    if (id < 0 || id >= (int32_t)b->ents.size()) return rt_set_error(RT_E_INVALID, "rt_builder_move: entity %d", id);
+    BEnt &e = b->ents[id];
+    // Entity._set_pos
+    if (e.type == RT_ENT_SPHERE) {
+        // SphereEntity._set_pos (src/entities/entity_sphere.ts:55-61): sphere_math.pos = p runs
+        // Sphere.update_cache (src/math/intersection.ts:94-97): _dot_pp anew, _radius_sq = r*r
+        // (the same value as before); SphereEntity._radius_sq is untouched
+        for (int i = 0; i < 3; i++) e.g[i] = pos[i];
+        e.g[4] = dot3(pos[0], pos[1], pos[2], pos[0], pos[1], pos[2]);
+    } else if (e.type == RT_ENT_BOX) {
+        for (int i = 0; i < 3; i++) e.g[i] = pos[i];   // BasicEntity._set_pos (src/entities/entity_basic.ts:38-42)
+    } else {
+        // FaceEntity._set_pos (raytracer.js_amd/js/raytracer.js): translate so the centroid lands on pos
+        double d[3];
+        for (int i = 0; i < 3; i++) d[i] = pos[i] - (e.g[i] + e.g[3 + i] + e.g[6 + i]) / 3;
+        for (int v = 0; v < 3; v++)
+            for (int i = 0; i < 3; i++) e.g[3 * v + i] += d[i];
+    }
+    // add_entity_to_octree(root, entity, flags) -> Entity.set_octree(fitting): Set.delete + Set.add
+    int fit;
+    int r = place(b, e, &fit);
+    if (r != RT_OK) return r;
+    BEnt &m = b->ents[id];
+    if (m.owner >= 0) {
+        std::vector<int> &set = b->nodes[m.owner].set;
+        set.erase(std::find(set.begin(), set.end(), id));
+    }
+    m.owner = fit;
+    b->nodes[fit].set.push_back(id);
+    return RT_OK;
+}
+
+extern "C" int rt_builder_set_shade(rt_builder *b, int32_t id, int32_t shade, int32_t substance)
+{
+    if (!b) return rt_set_error(RT_E_INVALID, "rt_builder_set_shade: null argument");
+    if (id < 0 || id >= (int32_t)b->ents.size()) return rt_set_error(RT_E_INVALID, "rt_builder_set_shade: entity %d", id);
+    b->ents[id].shade = shade;
+    b->ents[id].substance = substance;
     return RT_OK;
 }
 

@@ -186,49 +186,47 @@ struct Builder {
 
 }  // namespace
 
-// prim: all records in global list order (rank = index).  Rewrites `prim` into per-node cull
-// order, fills `bvh`, node_ent (4 ints per node) and the Set-order type prefix counts.
-int rt_build_cull(const rt_scene_desc *s, std::vector<RtPrim> &prim, std::vector<RtBvh> &bvh,
-                  std::vector<int32_t> &node_ent, std::vector<int32_t> &prefix, bool sah)
+// Cull scale of a scene: delta (AABB widening) and the SAH area clamp, from the root cube only, so
+// an incremental update rebuilds a node with the same constants as a full upload.
+void rt_cull_scale(const double root_pos[3], double root_size, double *delta, double *clampv)
 {
-    const int N = s->n_nodes;
-    double scale = fabs(s->node_size[0]);
-    for (int i = 0; i < 3; i++)
-        scale = std::max(scale, std::max(fabs(s->node_pos[i]), fabs(s->node_pos[i] + s->node_size[0])));
-    const double delta = ldexp(scale, -13);          // ~1.2e-4 x scene scale
-    node_ent.assign(4 * (size_t)N, 0);
-    prefix.assign(4 * (size_t)(s->n_list ? s->n_list : 1), 0);
-    bvh.clear();
-    std::vector<RtPrim> out(prim.size());
-    std::vector<Item> items;
-    for (int n = 0; n < N; n++) {
-        const int b = s->node_ent_begin[n], c = s->node_ent_count[n];
-        int cnt[3] = {0, 0, 0};
-        for (int k = b; k < b + c; k++) {
-            cnt[prim[k].meta & 3]++;
-            for (int t = 0; t < 3; t++) prefix[4 * (size_t)k + t] = cnt[t];
-        }
-        node_ent[4 * n] = b;
-        node_ent[4 * n + 1] = c;
-        node_ent[4 * n + 2] = -1;
-        if (c == 0) continue;
-        items.resize(c);
-        for (int k = 0; k < c; k++) {
-            prim_bounds(prim[b + k], delta, items[k]);
-            items[k].slot = k;
-        }
-        const int root = (int)bvh.size();
-        Builder B{&bvh, {}, &items, sah, 4 * scale, {}};
-        B.order.reserve(c);
-        B.emit(0, c);
-        const int end = (int)bvh.size();
-        for (int i = root; i < end; i++) {
-            if (bvh[i].skip >= end) bvh[i].skip = -1;
-            if (bvh[i].info >= 0) bvh[i].info = ((bvh[i].info >> 4) + b) << 4 | (bvh[i].info & 15);
-        }
-        for (int k = 0; k < c; k++) out[b + k] = prim[b + items[B.order[k]].slot];
-        node_ent[4 * n + 2] = root;
+    double scale = fabs(root_size);
+    for (int i = 0; i < 3; i++) scale = std::max(scale, std::max(fabs(root_pos[i]), fabs(root_pos[i] + root_size)));
+    *delta = ldexp(scale, -13);          // ~1.2e-4 x scene scale
+    *clampv = 4 * scale;
+}
+
+// One node's cull hierarchy.  `recs` are the node's c prim records in Set order (rank already
+// set); prim_out[0..c) receives them in cull (leaf) order, bvh_out[0..2c-1) the hierarchy, with
+// absolute prim slots (prim_base + k) in leaves and absolute skip pointers (bvh_base + i, -1 past
+// the end).  prefix_out[4k..4k+2] = #sph/#box/#tri among Set positions 0..k (stats).
+int rt_build_node_cull(const RtPrim *recs, int c, int prim_base, int bvh_base, double delta, double clampv,
+                       bool sah, RtPrim *prim_out, RtBvh *bvh_out, int32_t *prefix_out)
+{
+    int cnt[3] = {0, 0, 0};
+    for (int k = 0; k < c; k++) {
+        cnt[recs[k].meta & 3]++;
+        for (int t = 0; t < 3; t++) prefix_out[4 * (size_t)k + t] = cnt[t];
+        prefix_out[4 * (size_t)k + 3] = 0;
     }
-    prim.swap(out);
-    return RT_OK;
+    if (c == 0) return -1;
+    std::vector<Item> items(c);
+    for (int k = 0; k < c; k++) {
+        prim_bounds(recs[k], delta, items[k]);
+        items[k].slot = k;
+    }
+    std::vector<RtBvh> bvh;
+    bvh.reserve(2 * (size_t)c - 1);
+    Builder B{&bvh, {}, &items, sah, clampv, {}};
+    B.order.reserve(c);
+    B.emit(0, c);
+    const int end = (int)bvh.size();
+    for (int i = 0; i < end; i++) {
+        RtBvh n = bvh[i];
+        n.skip = n.skip >= end ? -1 : n.skip + bvh_base;
+        if (n.info >= 0) n.info = ((n.info >> 4) + prim_base) << 4 | (n.info & 15);
+        bvh_out[i] = n;
+    }
+    for (int k = 0; k < c; k++) prim_out[k] = recs[items[B.order[k]].slot];
+    return bvh_base;
 }

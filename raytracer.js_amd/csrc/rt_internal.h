@@ -38,6 +38,8 @@ struct alignas(16) RtBvh {
 };
 static_assert(sizeof(RtBvh) == 32, "RtBvh must stay 32 bytes");
 
+// Nodes live in stable slots (rt_scene.hip): slot 0 is the root; after incremental updates slot
+// order is no longer DFS order, node_dfs maps back.
 struct RtDevScene {
     const double *node_ps;      // [n_nodes*4]
     const int32_t *node_child;  // [n_nodes*8]
@@ -50,6 +52,7 @@ struct RtDevScene {
     const rt_shade *shades;     // [n_shades]
     const int32_t *ent_sub;     // [n_entities]
     const double *sub_ri;       // [n_substances]
+    const int32_t *node_dfs;    // [n_nodes] DFS pre-order id of each node slot (the reported node id)
     int32_t n_nodes, n_list, n_entities, n_shades, n_subs, n_bvh;
 };
 
@@ -73,6 +76,13 @@ struct RtFrameSetup {
 // Counter slots (rt_stats order).
 enum { CT_SEG, CT_RET, CT_SLOT, CT_LOC, CT_SPH, CT_BOX, CT_TRI, CT_HIT, CT_PRIM, CT_WARN, CT_FAULT,
        CT_CULL, CT_EXACT, CT_N };
+
+// The resident scene (rt_scene.hip): full upload or incremental update into stable device slots.
+struct RtSceneStore;
+RtSceneStore *rt_store_new(bool sah);
+void rt_store_free(RtSceneStore *st);
+int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, void *stream, RtDevScene *dev,
+                    bool *scatter, rt_update_stats *stats);
 
 // Kernel launchers (rt_kernels.hip).
 struct RtLaunch {

@@ -922,7 +922,7 @@ __device__ __forceinline__ void write_pixel(const RtLaunch &L, size_t pix, const
         px[k] = (float)v;
     }
     if (L.hit_entity) L.hit_entity[pix] = R.hit_ent;
-    if (L.hit_node) L.hit_node[pix] = R.hit_node;
+    if (L.hit_node) L.hit_node[pix] = R.hit_node >= 0 ? L.scene.node_dfs[R.hit_node] : R.hit_node;
     if (L.status) L.status[pix] = (uint8_t)R.status;
     if (R.status >= ST_FAULT && L.fault) atomicOr(L.fault, 1);
 }
@@ -1206,7 +1206,7 @@ __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, doub
         const int r = walker_next<INCL_UNDEF>(S, w, node, pt, po, c);
         if (r < 0) { *n_out = -1; return; }
         if (r == 0 || n >= max_out) break;
-        out_tree[n] = pt;
+        out_tree[n] = pt >= 0 ? S.node_dfs[pt] : pt;
         out_oct[n] = po == RT_OCT_UNDEF ? -1 : po;
         n++;
     }

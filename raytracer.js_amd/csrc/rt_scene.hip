@@ -1,0 +1,680 @@
+// rt_scene.hip — the resident scene behind rt_upload_scene / rt_update_scene.
+//
+// Device layout (RtDevScene, rt_internal.h), in stable slots:
+//   node slots   node_ps / node_child / node_up / node_ent / node_dfs.  A full upload numbers the
+//                slots in DFS pre-order; an update keeps every existing node in its slot and
+//                appends new ones, and node_dfs maps a slot to the DFS id the outputs report.
+//   list pool    prim / list_entity / list_prefix.  A node owns a region [lbeg, lbeg+lcap) holding
+//                its EntitySet: list_entity and list_prefix in Set order (Set rank = lbeg + position),
+//                the prim records in cull-leaf order.
+//   bvh pool     a node's cull hierarchy, 2*count-1 records in [bbeg, bbeg+bcap).
+// An update (a scene edit: add_entity_to_octree, Entity.set_octree, set_material; the reference
+// never removes nodes) rebuilds only the nodes whose list or member entities changed: in place
+// when they fit their regions, else at the end of the pool with slack.  Everything that changed
+// travels in one pinned staging copy and is put in place by one scatter kernel.  Regions left
+// behind are garbage until the next full upload compacts.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <new>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "rt.h"
+#include "rt_internal.h"
+#include "rt_jsnum.h"
+
+void rt_cull_scale(const double root_pos[3], double root_size, double *delta, double *clampv);
+int rt_build_node_cull(const RtPrim *recs, int c, int prim_base, int bvh_base, double delta, double clampv,
+                       bool sah, RtPrim *prim_out, RtBvh *bvh_out, int32_t *prefix_out);
+
+#define HIP_TRY(x)                                                                                \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) return rt_set_error(RT_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+enum Arr { A_NODE_PS, A_NODE_CHILD, A_NODE_UP, A_NODE_ENT, A_NODE_DFS, A_PRIM, A_BVH, A_LIST, A_PREFIX,
+           A_SHADES, A_ENT_SUB, A_SUB_RI, A_N };
+
+struct DevArr {
+    void *p = nullptr;
+    size_t cap = 0;          // bytes
+    // capacity >= bytes, keeping the first `keep` bytes.  Growth adds 1/8 + 64 KiB of headroom
+    // (or 1.5x), so small edits never reallocate (hipMalloc / hipFree cost milliseconds).
+    int reserve(size_t bytes, size_t keep, hipStream_t st)
+    {
+        if (bytes <= cap && p) return RT_OK;
+        const size_t nc = std::max(bytes + bytes / 8 + 65536, cap + cap / 2);
+        void *q = nullptr;
+        HIP_TRY(hipMalloc(&q, nc));
+        if (p && keep) HIP_TRY(hipMemcpyAsync(q, p, std::min(keep, cap), hipMemcpyDeviceToDevice, st));
+        if (p) {
+            HIP_TRY(hipStreamSynchronize(st));
+            (void)hipFree(p);
+        }
+        p = q;
+        cap = nc;
+        return RT_OK;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Chunk {
+    uint64_t dst, src, bytes;    // device address, staging offset, length (multiple of 4)
+};
+
+constexpr size_t PIECE = 16384;  // bytes per scatter block
+
+// One block per chunk piece: 4-byte words from the staging buffer to their device addresses.
+__global__ void __launch_bounds__(256) k_scene_patch(const Chunk *__restrict__ chunks, const uint8_t *__restrict__ stage)
+{
+    const Chunk ch = chunks[blockIdx.x];
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + ch.src);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(ch.dst);
+    const uint32_t n = (uint32_t)(ch.bytes >> 2);
+    for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+}
+
+using Key = std::array<uint64_t, 4>;
+struct KeyHash {
+    size_t operator()(const Key &k) const
+    {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (uint64_t v : k) h = rtjs::mix64(h ^ v);
+        return (size_t)h;
+    }
+};
+
+Key node_key(const rt_scene_desc *s, int n)
+{
+    Key k;
+    memcpy(&k[0], s->node_pos + 3 * (size_t)n, 24);
+    memcpy(&k[3], s->node_size + n, 8);
+    return k;
+}
+
+struct Slot {
+    int32_t lbeg, lcap, cnt, bbeg, bcap, broot;
+};
+
+// Node n's shape checks and index_within_parent; `report` sets the error message (only on the
+// calling thread: rt_set_error's message is thread-local).
+int check_node(const rt_scene_desc *s, int n, int32_t &oct, bool report)
+{
+    const int N = s->n_nodes, NL = s->n_list;
+    const int p = s->node_parent[n];
+    if (n > 0 && (p < 0 || p >= N))
+        return report ? rt_set_error(RT_E_INVALID, "rt_upload_scene: node %d parent %d", n, p) : RT_E_INVALID;
+    for (int k = 0; k < 8; k++) {
+        const int ch = s->node_child[8 * (size_t)n + k];
+        if (ch < -1 || ch >= N || ch == 0)
+            return report ? rt_set_error(RT_E_INVALID, "rt_upload_scene: node %d child %d", n, ch) : RT_E_INVALID;
+        if (ch > 0 && s->node_parent[ch] != n)
+            return report ? rt_set_error(RT_E_INVALID, "rt_upload_scene: child %d of %d has parent %d", ch, n,
+                                         s->node_parent[ch])
+                          : RT_E_INVALID;
+    }
+    if (n == 0) {
+        oct = RT_OCT_UNDEF;
+    } else {
+        // index_within_parent (src/octree_space.ts:113-125): geometric, never cached
+        const double sc = 2 / s->node_size[p];
+        const int32_t ix = rtjs::toint32((s->node_pos[3 * (size_t)n + 0] - s->node_pos[3 * (size_t)p + 0]) * sc);
+        const int32_t iy = rtjs::toint32((s->node_pos[3 * (size_t)n + 1] - s->node_pos[3 * (size_t)p + 1]) * sc);
+        const int32_t iz = rtjs::toint32((s->node_pos[3 * (size_t)n + 2] - s->node_pos[3 * (size_t)p + 2]) * sc);
+        const double idx = rtjs::octant_sum(ix, iy, iz);
+        oct = (idx >= 0 && idx <= 7) ? (int)idx : RT_OCT_BAD;
+    }
+    const int b = s->node_ent_begin[n], cnt = s->node_ent_count[n];
+    if (b < 0 || cnt < 0 || (long long)b + cnt > NL)
+        return report ? rt_set_error(RT_E_INVALID, "rt_upload_scene: node %d entity range", n) : RT_E_INVALID;
+    return RT_OK;
+}
+
+// Shape checks of rt_upload_scene, index_within_parent per node, and whether a rough mirror is
+// listed.  Large trees are checked by up to 8 host threads; the first bad node (lowest index) is
+// reported, as a serial pass would.
+int validate(const rt_scene_desc *s, std::vector<int32_t> &oct, bool &scatter)
+{
+    const int N = s->n_nodes, NL = s->n_list, NE = s->n_entities;
+    if (N < 1 || NL < 0 || NE < 0 || s->n_shades < 0 || s->n_substances < 0)
+        return rt_set_error(RT_E_INVALID, "rt_upload_scene: bad counts");
+    if (!s->node_pos || !s->node_size || !s->node_parent || !s->node_child || !s->node_ent_begin ||
+        !s->node_ent_count || (NL && !s->list_entity) ||
+        (NE && (!s->ent_type || !s->ent_geom || !s->ent_shade || !s->ent_substance)) ||
+        (s->n_shades && !s->shades) || (s->n_substances && !s->substance_ri))
+        return rt_set_error(RT_E_INVALID, "rt_upload_scene: null array");
+    if (s->node_parent[0] != -1) return rt_set_error(RT_E_INVALID, "rt_upload_scene: node 0 must be the root");
+    oct.resize(N);
+    const int T = N < (1 << 16) ? 1 : 8;
+    std::vector<int> first_bad(T, N);
+    auto work = [&](int t) {
+        const int lo = (int)((long long)N * t / T), hi = (int)((long long)N * (t + 1) / T);
+        for (int n = lo; n < hi; n++)
+            if (check_node(s, n, oct[n], false) != RT_OK) { first_bad[t] = n; return; }
+    };
+    if (T == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; t++) th.emplace_back(work, t);
+        for (std::thread &x : th) x.join();
+    }
+    const int bad = *std::min_element(first_bad.begin(), first_bad.end());
+    if (bad < N) return check_node(s, bad, oct[bad], true);
+    for (int e = 0; e < NE; e++) {
+        if (s->ent_type[e] < RT_ENT_SPHERE || s->ent_type[e] > RT_ENT_FACE)
+            return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d type", e);
+        if (s->ent_shade[e] < 0 || s->ent_shade[e] >= s->n_shades)
+            return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d shade", e);
+        if (s->ent_substance[e] < -1 || s->ent_substance[e] >= s->n_substances)
+            return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d substance", e);
+    }
+    scatter = false;
+    for (int k = 0; k < NL; k++) {
+        const int e = s->list_entity[k];
+        if (e < 0 || e >= NE) return rt_set_error(RT_E_INVALID, "rt_upload_scene: list entry %d entity %d", k, e);
+        const rt_shade &sh = s->shades[s->ent_shade[e]];
+        if (!sh.light && sh.response == RT_RESP_REFLECTION && sh.mirror && sh.roughness > 0.0) scatter = true;
+    }
+    return RT_OK;
+}
+
+// The exact-test record of entity e at Set rank `rank`.
+RtPrim make_rec(const rt_scene_desc *s, int e, int rank)
+{
+    const double *g = s->ent_geom + 9 * (size_t)e;
+    RtPrim p;
+    memset(&p, 0, sizeof p);
+    const int type = s->ent_type[e];
+    if (type == RT_ENT_SPHERE) {
+        p.g[0] = g[0]; p.g[1] = g[1]; p.g[2] = g[2];
+        p.g[3] = g[4];            // _dot_pp
+        p.g[4] = g[5];            // Sphere._radius_sq
+        p.g[5] = g[6];            // SphereEntity._radius_sq (is_within)
+        p.g[6] = 2 / g[3];        // 2 / diameter (normal scale)
+    } else if (type == RT_ENT_BOX) {
+        p.g[0] = g[0]; p.g[1] = g[1]; p.g[2] = g[2]; p.g[3] = g[3];
+    } else {
+        for (int i = 0; i < 3; i++) {
+            p.g[i] = g[i];
+            p.g[3 + i] = g[3 + i] - g[i];   // e1 = v1 - v0
+            p.g[6 + i] = g[6 + i] - g[i];   // e2 = v2 - v0
+        }
+    }
+    p.meta = type | (s->ent_shade[e] << 2);
+    p.rank = rank;
+    return p;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0)
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+struct RtSceneStore {
+    bool sah = true;
+    bool has = false;
+    double delta = 0, clampv = 0;
+    Key root{};
+    std::vector<Slot> slots;
+    std::unordered_map<Key, int32_t, KeyHash> slot_of;
+    // host mirrors of the device arrays (the diff base)
+    std::vector<double> m_ps;                          // 4 / slot
+    std::vector<int32_t> m_child, m_up, m_ent, m_dfs;  // 8, 2, 4, 1 / slot
+    std::vector<int32_t> m_order;                      // slot of each DFS id
+    std::vector<int32_t> m_list;                       // 1 / list-pool entry
+    std::vector<int32_t> m_type, m_shade, m_sub;       // 1 / entity
+    std::vector<double> m_geom;                        // 9 / entity
+    std::vector<rt_shade> m_shades;
+    std::vector<double> m_ri;
+    size_t list_used = 0, bvh_used = 0;
+    DevArr a[A_N];
+    // staging
+    uint8_t *pinned = nullptr;
+    size_t pinned_cap = 0;
+    DevArr dstage;
+    std::vector<uint8_t> stage;
+    struct Pending { int arr; size_t off, bytes, src; };
+    std::vector<Pending> pend;
+
+    ~RtSceneStore()
+    {
+        for (DevArr &d : a) d.release();
+        dstage.release();
+        if (pinned) (void)hipHostFree(pinned);
+    }
+
+    void add(int arr, size_t off, const void *src, size_t bytes)
+    {
+        if (!bytes) return;
+        size_t at = (stage.size() + 15) & ~(size_t)15;
+        stage.resize(at + bytes);
+        memcpy(stage.data() + at, src, bytes);
+        for (size_t o = 0; o < bytes; o += PIECE) pend.push_back({arr, off + o, std::min(PIECE, bytes - o), at + o});
+    }
+
+    // Patches for every run of records whose `w` elements differ between `nw` and `old`; then old = nw.
+    template <typename T>
+    void diff_runs(int arr, const std::vector<T> &nw, std::vector<T> &old, size_t w)
+    {
+        const size_t n = nw.size() / w, n_old = old.size() / w;
+        auto same = [&](size_t k) { return k < n_old && std::equal(&nw[k * w], &nw[k * w] + w, &old[k * w]); };
+        size_t i = 0;
+        while (i < n) {
+            if (same(i)) { i++; continue; }
+            size_t j = i + 1;
+            while (j < n && !same(j)) j++;
+            add(arr, i * w * sizeof(T), &nw[i * w], (j - i) * w * sizeof(T));
+            i = j;
+        }
+        old = nw;
+    }
+
+    // Patches for sorted, unique slots (runs of consecutive slots coalesced); rec = bytes per slot.
+    void add_slots(int arr, const std::vector<int32_t> &sl, const void *mirror, size_t rec)
+    {
+        const uint8_t *m = static_cast<const uint8_t *>(mirror);
+        size_t i = 0;
+        while (i < sl.size()) {
+            size_t j = i + 1;
+            while (j < sl.size() && sl[j] == sl[j - 1] + 1) j++;
+            add(arr, rec * (size_t)sl[i], m + rec * (size_t)sl[i], rec * (j - i));
+            i = j;
+        }
+    }
+
+    int flush(hipStream_t st, int64_t *bytes_out)
+    {
+        const size_t nch = pend.size();
+        if (!nch) return RT_OK;
+        const size_t tab = (stage.size() + 15) & ~(size_t)15, total = tab + nch * sizeof(Chunk);
+        if (total > pinned_cap) {
+            const size_t nc = std::max<size_t>(std::max(total, 2 * pinned_cap), 8u << 20);   // hipHostMalloc is slow
+            if (pinned) (void)hipHostFree(pinned);
+            pinned = nullptr;
+            pinned_cap = 0;
+            HIP_TRY(hipHostMalloc((void **)&pinned, nc, hipHostMallocDefault));
+            pinned_cap = nc;
+        }
+        int r = dstage.reserve(total, 0, st);
+        if (r != RT_OK) return r;
+        memcpy(pinned, stage.data(), stage.size());
+        Chunk *tabp = reinterpret_cast<Chunk *>(pinned + tab);
+        for (size_t k = 0; k < nch; k++)
+            tabp[k] = {(uint64_t)(uintptr_t)a[pend[k].arr].p + pend[k].off, pend[k].src, pend[k].bytes};
+        HIP_TRY(hipMemcpyAsync(dstage.p, pinned, total, hipMemcpyHostToDevice, st));
+        const uint8_t *dev = (const uint8_t *)dstage.p;
+        for (size_t k0 = 0; k0 < nch; k0 += 65535) {
+            const unsigned nb = (unsigned)std::min<size_t>(65535, nch - k0);
+            hipLaunchKernelGGL(k_scene_patch, dim3(nb), dim3(256), 0, st,
+                               reinterpret_cast<const Chunk *>(dev + tab) + k0, dev);
+            HIP_TRY(hipGetLastError());
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        *bytes_out += (int64_t)total;
+        stage.clear();
+        pend.clear();
+        return RT_OK;
+    }
+
+    // Device capacities for the current high-water marks, keeping what is resident.
+    int reserve_all(size_t n_slots, size_t n_ent, size_t n_shades, size_t n_ri, hipStream_t st, bool keep)
+    {
+        const size_t need[A_N] = {32 * n_slots, 32 * n_slots, 8 * n_slots, 16 * n_slots, 4 * n_slots,
+                                  sizeof(RtPrim) * list_used, sizeof(RtBvh) * bvh_used, 4 * list_used,
+                                  16 * list_used, sizeof(rt_shade) * n_shades, 4 * n_ent, 8 * n_ri};
+        for (int k = 0; k < A_N; k++) {
+            int r = a[k].reserve(need[k], keep ? a[k].cap : 0, st);
+            if (r != RT_OK) return r;
+        }
+        return RT_OK;
+    }
+
+    void fill(const rt_scene_desc *s, RtDevScene &d) const
+    {
+        d.node_ps = (const double *)a[A_NODE_PS].p;
+        d.node_child = (const int32_t *)a[A_NODE_CHILD].p;
+        d.node_up = (const int32_t *)a[A_NODE_UP].p;
+        d.node_ent = (const int32_t *)a[A_NODE_ENT].p;
+        d.node_dfs = (const int32_t *)a[A_NODE_DFS].p;
+        d.prim = (const RtPrim *)a[A_PRIM].p;
+        d.bvh = (const RtBvh *)a[A_BVH].p;
+        d.list_entity = (const int32_t *)a[A_LIST].p;
+        d.list_prefix = (const int32_t *)a[A_PREFIX].p;
+        d.shades = (const rt_shade *)a[A_SHADES].p;
+        d.ent_sub = (const int32_t *)a[A_ENT_SUB].p;
+        d.sub_ri = (const double *)a[A_SUB_RI].p;
+        d.n_nodes = (int32_t)slots.size();
+        d.n_list = (int32_t)list_used;
+        d.n_entities = s->n_entities;
+        d.n_shades = s->n_shades;
+        d.n_subs = s->n_substances;
+        d.n_bvh = (int32_t)bvh_used;
+    }
+
+    void entity_mirrors(const rt_scene_desc *s)
+    {
+        const size_t NE = (size_t)s->n_entities;
+        m_type.assign(s->ent_type, s->ent_type + NE);
+        m_shade.assign(s->ent_shade, s->ent_shade + NE);
+        m_sub.assign(s->ent_substance, s->ent_substance + NE);
+        m_geom.assign(s->ent_geom, s->ent_geom + 9 * NE);
+        m_shades.assign(s->shades, s->shades + s->n_shades);
+        m_ri.assign(s->substance_ri, s->substance_ri + s->n_substances);
+    }
+
+    // Full upload: slots in DFS order, regions packed exactly.
+    int full(const rt_scene_desc *s, const std::vector<int32_t> &oct, hipStream_t st, rt_update_stats &us)
+    {
+        const int N = s->n_nodes, NL = s->n_list;
+        const auto t0 = std::chrono::steady_clock::now();
+        has = false;
+        rt_cull_scale(s->node_pos, s->node_size[0], &delta, &clampv);
+        root = node_key(s, 0);
+        slots.assign(N, Slot{});
+        slot_of.clear();
+        slot_of.reserve((size_t)N * 2);
+        m_ps.assign(4 * (size_t)N, 0);
+        m_child.assign(s->node_child, s->node_child + 8 * (size_t)N);
+        m_up.assign(2 * (size_t)N, 0);
+        m_ent.assign(4 * (size_t)N, 0);
+        m_dfs.resize(N);
+        m_order.resize(N);
+        m_list.resize(NL);
+        size_t nb = 0;
+        for (int n = 0; n < N; n++) nb += s->node_ent_count[n] ? 2 * (size_t)s->node_ent_count[n] - 1 : 0;
+        std::vector<RtPrim> prim((size_t)std::max(NL, 1)), recs;
+        std::vector<RtBvh> bvh(std::max<size_t>(nb, 1));
+        std::vector<int32_t> prefix(4 * (size_t)std::max(NL, 1));
+        size_t lb = 0, bb = 0;
+        for (int n = 0; n < N; n++) {
+            for (int i = 0; i < 3; i++) m_ps[4 * n + i] = s->node_pos[3 * n + i];
+            m_ps[4 * n + 3] = s->node_size[n];
+            m_up[2 * n] = n == 0 ? -1 : s->node_parent[n];
+            m_up[2 * n + 1] = oct[n];
+            m_dfs[n] = n;
+            m_order[n] = n;
+            slot_of.emplace(node_key(s, n), n);
+            const int b = s->node_ent_begin[n], c = s->node_ent_count[n];
+            recs.resize(c);
+            for (int k = 0; k < c; k++) {
+                m_list[lb + k] = s->list_entity[b + k];
+                recs[k] = make_rec(s, s->list_entity[b + k], (int)(lb + k));
+            }
+            const int broot = c ? rt_build_node_cull(recs.data(), c, (int)lb, (int)bb, delta, clampv, sah,
+                                                     &prim[lb], &bvh[bb], &prefix[4 * lb])
+                                : -1;
+            slots[n] = {(int32_t)lb, c, c, (int32_t)bb, c ? 2 * c - 1 : 0, broot};
+            m_ent[4 * n] = (int32_t)lb;
+            m_ent[4 * n + 1] = c;
+            m_ent[4 * n + 2] = broot;
+            lb += c;
+            bb += c ? 2 * (size_t)c - 1 : 0;
+        }
+        if ((int)slot_of.size() != N) return rt_set_error(RT_E_INVALID, "rt_upload_scene: two nodes share a cube");
+        list_used = lb;
+        bvh_used = bb;
+        entity_mirrors(s);
+        us.host_ms = ms_since(t0);
+        int r = reserve_all(N, s->n_entities, s->n_shades, s->n_substances, st, false);
+        if (r != RT_OK) return r;
+        const void *src[A_N] = {m_ps.data(), m_child.data(), m_up.data(), m_ent.data(), m_dfs.data(), prim.data(),
+                                bvh.data(), m_list.data(), prefix.data(), s->shades, s->ent_substance, s->substance_ri};
+        const size_t bytes[A_N] = {32 * (size_t)N, 32 * (size_t)N, 8 * (size_t)N, 16 * (size_t)N, 4 * (size_t)N,
+                                   sizeof(RtPrim) * lb, sizeof(RtBvh) * bb, 4 * lb, 16 * lb,
+                                   sizeof(rt_shade) * (size_t)s->n_shades, 4 * (size_t)s->n_entities,
+                                   8 * (size_t)s->n_substances};
+        for (int k = 0; k < A_N; k++) {
+            if (!bytes[k]) continue;
+            HIP_TRY(hipMemcpyAsync(a[k].p, src[k], bytes[k], hipMemcpyHostToDevice, st));
+            us.bytes += (int64_t)bytes[k];
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        us.full = 1;
+        us.dirty_nodes = N;
+        us.changed_entities = s->n_entities;
+        has = true;
+        return RT_OK;
+    }
+
+    // Incremental update; returns 1 when the scene is not an edit of the resident one (caller does full).
+    int update(const rt_scene_desc *s, const std::vector<int32_t> &oct, hipStream_t st, rt_update_stats &us)
+    {
+        const int N = s->n_nodes, NL = s->n_list, NE = s->n_entities;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (!has || node_key(s, 0) != root || NE < (int)m_type.size()) return 1;
+        // 1. node slots.  Old nodes keep their relative DFS order (nodes are only ever inserted), so
+        // one merge pass over the old DFS sequence matches them; anything else falls back to the
+        // cube -> slot hash.
+        const size_t n_old = slots.size();
+        std::vector<int32_t> slot_of_dfs(N);
+        size_t n_slots = n_old, i = 0;
+        for (int n = 0; n < N; n++) {
+            if (i < n_old) {
+                const int32_t sl = m_order[i];
+                if (memcmp(&m_ps[4 * (size_t)sl], s->node_pos + 3 * (size_t)n, 24) == 0 &&
+                    memcmp(&m_ps[4 * (size_t)sl + 3], s->node_size + n, 8) == 0) {
+                    slot_of_dfs[n] = sl;
+                    i++;
+                    continue;
+                }
+            }
+            slot_of_dfs[n] = (int32_t)n_slots++;
+        }
+        if (i != n_old) {
+            std::vector<char> seen(n_old, 0);
+            size_t n_seen = 0;
+            n_slots = n_old;
+            for (int n = 0; n < N; n++) {
+                auto it = slot_of.find(node_key(s, n));
+                if (it != slot_of.end() && it->second < (int32_t)n_old) {
+                    if (seen[it->second]) return rt_set_error(RT_E_INVALID, "rt_update_scene: two nodes share a cube");
+                    seen[it->second] = 1;
+                    n_seen++;
+                    slot_of_dfs[n] = it->second;
+                } else {
+                    slot_of_dfs[n] = (int32_t)n_slots++;
+                }
+            }
+            if (n_seen != n_old) return 1;          // a node disappeared: not an edit
+        }
+        const int new_nodes = (int)(n_slots - n_old);
+        // 2. entities
+        const size_t ne_old = m_type.size();
+        std::vector<char> chg(NE, 1);
+        int n_chg = 0;
+        for (size_t e = 0; e < ne_old; e++) {
+            chg[e] = m_type[e] != s->ent_type[e] || m_shade[e] != s->ent_shade[e] ||
+                     memcmp(&m_geom[9 * e], s->ent_geom + 9 * e, 72) != 0;
+            n_chg += chg[e] || m_sub[e] != s->ent_substance[e];
+        }
+        n_chg += (int)(NE - ne_old);
+        // 3. dirty nodes and their regions (decided before any capacity is reserved)
+        struct Dirty { int n, sl; };
+        std::vector<Dirty> dirty;
+        slots.resize(n_slots, Slot{0, 0, 0, 0, 0, -1});   // a full upload (return 1) reassigns them
+        size_t lu = list_used, bu = bvh_used, dirty_list = 0;
+        int moved = 0;
+        for (int n = 0; n < N; n++) {
+            const int sl = slot_of_dfs[n];
+            const int b = s->node_ent_begin[n], c = s->node_ent_count[n];
+            Slot &S = slots[sl];
+            bool d = sl >= (int)n_old || c != S.cnt ||
+                     (c && memcmp(&m_list[S.lbeg], s->list_entity + b, 4 * (size_t)c) != 0);
+            for (int k = 0; !d && k < c; k++) d = chg[s->list_entity[b + k]];
+            if (!d) continue;
+            dirty.push_back({n, sl});
+            dirty_list += c;
+            if (c > S.lcap) {
+                moved += sl < (int)n_old;
+                S.lcap = c + c / 2 + 2;
+                S.lbeg = (int32_t)lu;
+                lu += S.lcap;
+                S.bcap = 2 * S.lcap - 1;
+                S.bbeg = (int32_t)bu;
+                bu += S.bcap;
+            }
+        }
+        // most of the scene changed, or the pools are mostly garbage: compact with a full upload
+        if (dirty_list > (size_t)NL / 2 + 4096 || lu > 2 * (size_t)NL + 65536) return 1;
+        // 4. capacities (keeping the resident contents), then the patches
+        list_used = lu;
+        bvh_used = bu;
+        int r = reserve_all(n_slots, NE, s->n_shades, s->n_substances, st, true);
+        if (r != RT_OK) return r;
+        m_list.resize(lu, -1);
+        std::vector<RtPrim> recs, prim;
+        std::vector<RtBvh> bvh;
+        std::vector<int32_t> prefix;
+        m_ent.resize(4 * n_slots, 0);
+        for (const Dirty &dd : dirty) {
+            const int b = s->node_ent_begin[dd.n], c = s->node_ent_count[dd.n];
+            Slot &S = slots[dd.sl];
+            recs.resize(c);
+            prim.resize(c);
+            bvh.resize(c ? 2 * (size_t)c - 1 : 0);
+            prefix.resize(4 * (size_t)c);
+            for (int k = 0; k < c; k++) {
+                m_list[S.lbeg + k] = s->list_entity[b + k];
+                recs[k] = make_rec(s, s->list_entity[b + k], S.lbeg + k);
+            }
+            S.cnt = c;
+            S.broot = c ? rt_build_node_cull(recs.data(), c, S.lbeg, S.bbeg, delta, clampv, sah, prim.data(),
+                                             bvh.data(), prefix.data())
+                        : -1;
+            add(A_PRIM, sizeof(RtPrim) * (size_t)S.lbeg, prim.data(), sizeof(RtPrim) * (size_t)c);
+            add(A_BVH, sizeof(RtBvh) * (size_t)S.bbeg, bvh.data(), sizeof(RtBvh) * bvh.size());
+            add(A_LIST, 4 * (size_t)S.lbeg, &m_list[S.lbeg], 4 * (size_t)c);
+            add(A_PREFIX, 16 * (size_t)S.lbeg, prefix.data(), 16 * (size_t)c);
+            m_ent[4 * dd.sl] = S.lbeg;
+            m_ent[4 * dd.sl + 1] = c;
+            m_ent[4 * dd.sl + 2] = S.broot;
+            m_ent[4 * dd.sl + 3] = 0;
+        }
+        // node records: new slots, and the existing parents that gained a child (an existing node's
+        // cube, parent and octant never change); node_dfs wherever the DFS numbering shifted
+        std::vector<int32_t> touched;                 // slots whose ps / child / up records are rewritten
+        m_ps.resize(4 * n_slots);
+        m_child.resize(8 * n_slots);
+        m_up.resize(2 * n_slots);
+        std::vector<int32_t> n_dfs(m_dfs);
+        n_dfs.resize(n_slots);
+        m_order.resize(N);
+        for (int n = 0; n < N; n++) {
+            const int sl = slot_of_dfs[n];
+            n_dfs[sl] = n;
+            m_order[n] = sl;
+            if (sl < (int)n_old) continue;
+            touched.push_back(sl);
+            for (int k = 0; k < 3; k++) m_ps[4 * (size_t)sl + k] = s->node_pos[3 * (size_t)n + k];
+            m_ps[4 * (size_t)sl + 3] = s->node_size[n];
+            m_up[2 * (size_t)sl] = n == 0 ? -1 : slot_of_dfs[s->node_parent[n]];
+            m_up[2 * (size_t)sl + 1] = oct[n];
+            if (n > 0 && slot_of_dfs[s->node_parent[n]] < (int)n_old) touched.push_back(slot_of_dfs[s->node_parent[n]]);
+            slot_of.emplace(node_key(s, n), sl);
+        }
+        std::sort(touched.begin(), touched.end());
+        touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+        std::vector<int32_t> dfs_of_slot(n_slots);
+        for (int n = 0; n < N; n++) dfs_of_slot[slot_of_dfs[n]] = n;
+        for (int32_t sl : touched) {
+            const int n = dfs_of_slot[sl];
+            for (int k = 0; k < 8; k++) {
+                const int ch = s->node_child[8 * (size_t)n + k];
+                m_child[8 * (size_t)sl + k] = ch < 0 ? -1 : slot_of_dfs[ch];
+            }
+        }
+        add_slots(A_NODE_PS, touched, m_ps.data(), 4 * sizeof(double));
+        add_slots(A_NODE_CHILD, touched, m_child.data(), 8 * sizeof(int32_t));
+        add_slots(A_NODE_UP, touched, m_up.data(), 2 * sizeof(int32_t));
+        diff_runs(A_NODE_DFS, n_dfs, m_dfs, 1);
+        std::vector<int32_t> ent_slots;
+        ent_slots.reserve(dirty.size());
+        for (const Dirty &dd : dirty) ent_slots.push_back(dd.sl);
+        std::sort(ent_slots.begin(), ent_slots.end());
+        add_slots(A_NODE_ENT, ent_slots, m_ent.data(), 4 * sizeof(int32_t));
+        // entity substances and the shade / substance tables
+        std::vector<int32_t> n_sub(s->ent_substance, s->ent_substance + NE);
+        diff_runs(A_ENT_SUB, n_sub, m_sub, 1);
+        if (m_shades.size() != (size_t)s->n_shades ||
+            (s->n_shades && memcmp(m_shades.data(), s->shades, sizeof(rt_shade) * s->n_shades) != 0)) {
+            m_shades.assign(s->shades, s->shades + s->n_shades);
+            add(A_SHADES, 0, m_shades.data(), sizeof(rt_shade) * m_shades.size());
+        }
+        if (m_ri.size() != (size_t)s->n_substances ||
+            (s->n_substances && memcmp(m_ri.data(), s->substance_ri, 8 * (size_t)s->n_substances) != 0)) {
+            m_ri.assign(s->substance_ri, s->substance_ri + s->n_substances);
+            add(A_SUB_RI, 0, m_ri.data(), 8 * m_ri.size());
+        }
+        m_type.assign(s->ent_type, s->ent_type + NE);
+        m_shade.assign(s->ent_shade, s->ent_shade + NE);
+        m_geom.assign(s->ent_geom, s->ent_geom + 9 * (size_t)NE);
+        us.host_ms += ms_since(t0);
+        if ((r = flush(st, &us.bytes)) != RT_OK) {
+            has = false;                            // the device copy is no longer known
+            return r;
+        }
+        us.full = 0;
+        us.dirty_nodes = (int32_t)dirty.size();
+        us.new_nodes = new_nodes;
+        us.moved_regions = moved;
+        us.changed_entities = n_chg;
+        return RT_OK;
+    }
+};
+
+RtSceneStore *rt_store_new(bool sah)
+{
+    RtSceneStore *st = new (std::nothrow) RtSceneStore();
+    if (st) st->sah = sah;
+    return st;
+}
+
+void rt_store_free(RtSceneStore *st) { delete st; }
+
+int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, void *stream, RtDevScene *dev,
+                    bool *scatter, rt_update_stats *stats)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    rt_update_stats us;
+    memset(&us, 0, sizeof us);
+    std::vector<int32_t> oct;
+    bool sc = false;
+    int r = validate(s, oct, sc);
+    if (r != RT_OK) return r;
+    const double validate_ms = ms_since(t0);
+    hipStream_t hs = (hipStream_t)stream;
+    r = 1;
+    if (incremental) {
+        HIP_TRY(hipDeviceSynchronize());            // no frame may read the scene while it changes
+        r = st->update(s, oct, hs, us);
+        if (r < 0) return r;
+    }
+    if (r == 1) {
+        memset(&us, 0, sizeof us);
+        r = st->full(s, oct, hs, us);
+        if (r != RT_OK) return r;
+    }
+    us.host_ms += validate_ms;
+    st->fill(s, *dev);
+    *scatter = sc;
+    us.total_ms = ms_since(t0);
+    if (stats) *stats = us;
+    return RT_OK;
+}

@@ -172,7 +172,10 @@ napi_value Destroy(napi_env env, napi_callback_info info)
     return nullptr;
 }
 
-napi_value UploadScene(napi_env env, napi_callback_info info)
+napi_value set_num(napi_env env, napi_value obj, const char *k, double v);
+
+// uploadScene(ctx, scene) / updateScene(ctx, scene) -> stats: the flattened scene as typed arrays.
+napi_value scene_call(napi_env env, napi_callback_info info, bool update)
 {
     size_t argc = 2;
     napi_value argv[2];
@@ -237,9 +240,27 @@ napi_value UploadScene(napi_env env, napi_callback_info info)
     d.ent_substance = (const int32_t *)esub.data;
     d.shades = shades.data();
     d.substance_ri = (const double *)ri.data;
-    if (throw_rc(env, rt_upload_scene(ctx, &d))) return nullptr;
-    return nullptr;
+    if (!update) {
+        throw_rc(env, rt_upload_scene(ctx, &d));
+        return nullptr;
+    }
+    rt_update_stats st;
+    if (throw_rc(env, rt_update_scene(ctx, &d, &st))) return nullptr;
+    napi_value o;
+    napi_create_object(env, &o);
+    set_num(env, o, "full", st.full);
+    set_num(env, o, "dirty_nodes", st.dirty_nodes);
+    set_num(env, o, "new_nodes", st.new_nodes);
+    set_num(env, o, "moved_regions", st.moved_regions);
+    set_num(env, o, "changed_entities", st.changed_entities);
+    set_num(env, o, "bytes", (double)st.bytes);
+    set_num(env, o, "host_ms", st.host_ms);
+    set_num(env, o, "total_ms", st.total_ms);
+    return o;
 }
+
+napi_value UploadScene(napi_env env, napi_callback_info info) { return scene_call(env, info, false); }
+napi_value UpdateScene(napi_env env, napi_callback_info info) { return scene_call(env, info, true); }
 
 napi_value set_num(napi_env env, napi_value obj, const char *k, double v)
 {
@@ -348,6 +369,7 @@ napi_value Init(napi_env env, napi_value exports)
         {"create", nullptr, Create, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"destroy", nullptr, Destroy, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"uploadScene", nullptr, UploadScene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"updateScene", nullptr, UpdateScene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"traceFrame", nullptr, TraceFrame, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"lastError", nullptr, LastError, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"abiVersion", nullptr, AbiVersion, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -78,8 +78,11 @@ function material_fields(m) {
  * Flatten an EntityOtree (the root the Raytracer holds) into the rt_scene_desc arrays: nodes in DFS
  * pre-order with children 0..7 (Octree.get, src/octree.ts:51-54), each node's EntitySet in
  * insertion order (src/octree_entity.ts:32-49).  Returns {arrays..., entities, substances}.
+ * With `prev` (an earlier result for the same Raytracer), entity, shade and substance indices stay
+ * stable — known objects keep their index, new ones are appended — which rt_update_scene needs to
+ * send only what changed.
  */
-function serialize_scene(otree, default_substance) {
+function serialize_scene(otree, default_substance, prev) {
 	if (otree.parent != undefined) {
 		const err = new Error('raytracer.js_amd: the Raytracer octree has a parent (it grew outward); not supported');
 		err.code = 'RT_E_UNSUPPORTED';
@@ -100,8 +103,10 @@ function serialize_scene(otree, default_substance) {
 	const node_pos = new Float64Array(3 * n), node_size = new Float64Array(n);
 	const node_parent = new Int32Array(n), node_child = new Int32Array(8 * n).fill(-1);
 	const node_ent_begin = new Int32Array(n), node_ent_count = new Int32Array(n);
-	const entities = [], ent_index = new Map(), list = [];
-	const substances = [], sub_index = new Map();
+	const entities = prev ? prev.entities.slice() : [], list = [];
+	const ent_index = prev ? new Map(prev._maps.ent_index) : new Map();
+	const substances = prev ? prev.substances.slice() : [];
+	const sub_index = prev ? new Map(prev._maps.sub_index) : new Map();
 	const sub_of = (s) => {
 		if (s == undefined) return -1;
 		if (!sub_index.has(s)) { sub_index.set(s, substances.length); substances.push(s); }
@@ -134,7 +139,9 @@ function serialize_scene(otree, default_substance) {
 	const ne = entities.length;
 	const ent_type = new Int32Array(ne), ent_geom = new Float64Array(9 * ne);
 	const ent_shade = new Int32Array(ne), ent_substance = new Int32Array(ne);
-	const shades = [], shade_index = new Map();
+	const shades = prev ? prev._maps.shades.slice() : [];
+	const shade_index = new Map();
+	if (prev) for (const [m, per] of prev._maps.shade_index) shade_index.set(m, new Map(per));
 	for (let i = 0; i < ne; i++) {
 		const e = entities[i];
 		const kind = entity_kind(e);
@@ -165,11 +172,14 @@ function serialize_scene(otree, default_substance) {
 		if (!per_mat) { per_mat = new Map(); shade_index.set(m, per_mat); }
 		if (!per_mat.has(tex)) {
 			per_mat.set(tex, shades.length);
-			shades.push(Object.assign(material_fields(m), { rgb: solid_color(tex, 'entity texture') }));
+			shades.push(null);
 		}
 		ent_shade[i] = per_mat.get(tex);
 		ent_substance[i] = sub_of(e.get_substance());
 	}
+	// every (material, texture) row is re-read: a host may have edited a material in place
+	for (const [m, per] of shade_index)
+		for (const [tex, i] of per) shades[i] = Object.assign(material_fields(m), { rgb: solid_color(tex, 'entity texture') });
 	const def_sub = sub_of(default_substance);
 	const ns = shades.length;
 	const shade_response = new Int32Array(ns), shade_light = new Int32Array(ns), shade_mirror = new Int32Array(ns);
@@ -184,7 +194,8 @@ function serialize_scene(otree, default_substance) {
 		node_pos, node_size, node_parent, node_child, node_ent_begin, node_ent_count,
 		list_entity: new Int32Array(list), ent_type, ent_geom, ent_shade, ent_substance,
 		shade_response, shade_light, shade_mirror, shade_roughness, shade_rgb, substance_ri,
-		entities, substances, default_substance_index: def_sub
+		entities, substances, default_substance_index: def_sub,
+		_maps: { ent_index, sub_index, shades, shade_index }
 	};
 }
 
@@ -228,8 +239,10 @@ class Raytracer {
 	get tree() { return this.otree; }
 	get rng() { return this._rng; }
 
-	/** Re-flatten the octree before the next frame (call after adding/moving entities). */
-	invalidate_scene() { this._scene = null; }
+	/** Re-flatten the octree before the next frame (call after adding / moving entities or changing
+	 * materials).  The GPU copy is then updated incrementally (rt_update_scene): only the nodes
+	 * whose EntitySet or member entities changed are rebuilt and sent; `last_update` reports it. */
+	invalidate_scene() { this._dirty = true; }
 
 	/** Release the GPU context now instead of at garbage collection. */
 	close() {
@@ -242,7 +255,11 @@ class Raytracer {
 		if (!this._scene) {
 			this._scene = serialize_scene(this.otree, this.config.default_substance);
 			a.uploadScene(this._ctx, this._scene);
+		} else if (this._dirty) {
+			this._scene = serialize_scene(this.otree, this.config.default_substance, this._scene);
+			this.last_update = a.updateScene(this._ctx, this._scene);
 		}
+		this._dirty = false;
 		return this._scene;
 	}
 

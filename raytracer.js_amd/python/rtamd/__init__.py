@@ -111,6 +111,52 @@ def _desc_to_arrays(d):
         substance_ri=arr(d.substance_ri, d.n_substances, np.float64))
 
 
+class Builder:
+    """A live native scene (rt_builder_*): add / move / re-shade entities, then linearise."""
+
+    def __init__(self, root_pos=(0.0, 0.0, 0.0), root_size=1.0, shades=None, substances=None):
+        self.L = load_library()
+        b = C.c_void_p()
+        _check(self.L.rt_builder_create((C.c_double * 3)(*root_pos), float(root_size), C.byref(b)))
+        self.h = b
+        self.shades = np.zeros(0, abi.SHADE_DTYPE) if shades is None else np.ascontiguousarray(shades, abi.SHADE_DTYPE)
+        self.substances = np.zeros(0) if substances is None else np.ascontiguousarray(substances, np.float64)
+
+    @classmethod
+    def from_spec(cls, spec):
+        b = cls(spec.root_pos, spec.root_size, spec.shades, spec.substances)
+        b.add(spec.entities)
+        return b
+
+    def close(self):
+        if self.h:
+            self.L.rt_builder_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add(self, entities):
+        ents = np.ascontiguousarray(entities, dtype=abi.ENTITY_DTYPE)
+        _check(self.L.rt_builder_add_many(self.h, ents.ctypes.data_as(C.POINTER(abi.rt_entity_in)), len(ents)))
+
+    def move(self, entity_id, pos):
+        _check(self.L.rt_builder_move(self.h, int(entity_id), (C.c_double * 3)(*[float(x) for x in pos])))
+
+    def set_shade(self, entity_id, shade, substance):
+        _check(self.L.rt_builder_set_shade(self.h, int(entity_id), int(shade), int(substance)))
+
+    def arrays(self):
+        d = abi.rt_scene_desc()
+        _check(self.L.rt_builder_desc(self.h, self.shades.ctypes.data_as(C.POINTER(abi.rt_shade)), len(self.shades),
+                                      self.substances.ctypes.data_as(C.POINTER(C.c_double)), len(self.substances),
+                                      C.byref(d)))
+        return _desc_to_arrays(d)
+
+
 def build_scene(spec):
     """Native add_entity_to_octree over spec.entities (in order) → SceneArrays (linearised)."""
     L = load_library()
@@ -155,6 +201,13 @@ class Context:
     def upload(self, scene):
         self.scene = scene
         _check(self.L.rt_upload_scene(self.h, C.byref(scene.desc())))
+
+    def update(self, scene):
+        """rt_update_scene: incremental re-upload of an edited scene; returns rt_update_stats."""
+        self.scene = scene
+        st = abi.rt_update_stats()
+        _check(self.L.rt_update_scene(self.h, C.byref(scene.desc()), C.byref(st)))
+        return st
 
     def trace_frame(self, cam, cfg, rgb=None, ids=True, stats=True, allow_fault=False):
         P = cam.width * cam.height

@@ -89,6 +89,14 @@ class rt_exposure_stats(C.Structure):
 RT_TONEMAP_IDENTITY, RT_TONEMAP_STDDEV, RT_TONEMAP_ABSDEV = 0, 1, 2
 
 
+class rt_update_stats(C.Structure):
+    _fields_ = [("full", _i), ("dirty_nodes", _i), ("new_nodes", _i), ("moved_regions", _i),
+                ("changed_entities", _i), ("pad_", _i), ("bytes", C.c_int64), ("host_ms", _d), ("total_ms", _d)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad_"}
+
+
 class rt_create_desc(C.Structure):
     _fields_ = [("device", _i), ("flags", _i)]
 
@@ -108,7 +116,7 @@ EXPORTS = ("rt_create", "rt_destroy", "rt_last_error", "rt_abi_version", "rt_upl
            "rt_trace_frame", "rt_trace_rows_device", "rt_kernel_times", "rt_debug_walk",
            "rt_debug_camera_dirs", "rt_builder_create", "rt_builder_destroy", "rt_builder_add",
            "rt_builder_add_many", "rt_builder_desc", "rt_exposure_stats_device", "rt_tonemap_device",
-           "rt_tonemap_range")
+           "rt_tonemap_range", "rt_update_scene", "rt_builder_move", "rt_builder_set_shade")
 
 
 def declare(lib):
@@ -137,6 +145,9 @@ def declare(lib):
     lib.rt_exposure_stats_device.argtypes = [vp, vp, C.c_int64, vp, P(rt_exposure_stats)]
     lib.rt_tonemap_device.argtypes = [vp, vp, C.c_int64, _d, _d, vp, vp]
     lib.rt_tonemap_range.argtypes = [_i, P(rt_exposure_stats), _i, _d, _d, _pd]
+    lib.rt_update_scene.argtypes = [vp, P(rt_scene_desc), P(rt_update_stats)]
+    lib.rt_builder_move.argtypes = [vp, _i, _pd]
+    lib.rt_builder_set_shade.argtypes = [vp, _i, _i, _i]
     return lib
 
 

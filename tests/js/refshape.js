@@ -86,7 +86,7 @@ function inflate(sc) {
 		const b = sc.node_ent_begin[k], c = sc.node_ent_count[k];
 		for (let j = b; j < b + c; j++) nodes[k].value.set.add(ents[sc.list_entity[j]]);
 	}
-	return { root: nodes[0], entities: ents, substances: subs };
+	return { root: nodes[0], nodes, entities: ents, substances: subs };
 }
 
 /** Camera-shaped object from an rt_camera_desc-like record. */

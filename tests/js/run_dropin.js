@@ -1,8 +1,13 @@
 /*
- * run_dropin.js <scene.json> <out_prefix> [--serialize-only] [--scatter <seed>]
+ * run_dropin.js <scene.json> <out_prefix> [--serialize-only] [--scatter <seed>] [--edit A B C]
  * Builds reference-shaped objects, checks serialize_scene() reproduces the linearised arrays, and
  * (unless --serialize-only) renders one frame with the drop-in Raytracer into ExposureBuffer.pixels.
  * --scatter: rough mirrors with options.scatter = 'counter', the rng's one draw = seed / 2^53.
+ * --edit A B C: after the first frame, edit the live scene the way a host program does and render
+ *   again into <out_prefix>.2.* (the resident scene is updated incrementally, rt_update_scene):
+ *   sphere A is moved to (0.5, 0.5, 0.8) (Entity._set_pos + Set.delete / Set.add into the root's
+ *   EntitySet, which is where add_entity_to_octree files a cube straddling the centre planes), and
+ *   entity B takes entity C's material and texture (set_material / set_texture).
  */
 'use strict';
 const fs = require('fs');
@@ -59,5 +64,33 @@ fs.writeFileSync(out_prefix + '.ent', Buffer.from(ids.buffer));
 fs.writeFileSync(out_prefix + '.node', Buffer.from(tracer.last_hit_node.buffer));
 fs.writeFileSync(out_prefix + '.status', Buffer.from(tracer.last_status.buffer));
 fs.writeFileSync(out_prefix + '.json', JSON.stringify({ stats: tracer.last_stats, wall_ms: Number(t1 - t0) / 1e6 }));
+
+function write_frame(prefix, extra) {
+	const ids2 = Int32Array.from(tracer.last_hit_entity, (i) => (i >= 0 ? tracer._scene.entities[i].__orig_id : i));
+	fs.writeFileSync(prefix + '.rgb', Buffer.from(eb.pixels.buffer));
+	fs.writeFileSync(prefix + '.ent', Buffer.from(ids2.buffer));
+	fs.writeFileSync(prefix + '.node', Buffer.from(tracer.last_hit_node.buffer));
+	fs.writeFileSync(prefix + '.status', Buffer.from(tracer.last_status.buffer));
+	fs.writeFileSync(prefix + '.json', JSON.stringify(Object.assign({ stats: tracer.last_stats }, extra)));
+}
+
+const ei = process.argv.indexOf('--edit');
+if (ei > 0) {
+	const [A, B, C] = process.argv.slice(ei + 1, ei + 4).map(Number);
+	const ea = world.entities[A], eb2 = world.entities[B], ec = world.entities[C];
+	const home = world.nodes.find((t) => t.value.set.has(ea));
+	home.value.set.delete(ea);                                   // Entity.set_octree: Set.delete ...
+	const p = [0.5, 0.5, 0.8];
+	ea.pos = { v: p };                                           // SphereEntity._set_pos
+	ea.sphere_math._pos = ea.pos;                                //  -> Sphere.update_cache
+	ea.sphere_math._dot_pp = ((0 + p[0] * p[0]) + p[1] * p[1]) + p[2] * p[2];
+	ea.sphere_math._radius_sq = ea.sphere_math._radius * ea.sphere_math._radius;
+	world.root.value.set.add(ea);                                // ... Set.add (to the end)
+	eb2.material = ec.material;                                  // set_material
+	eb2.texture = ec.texture;                                    // set_texture
+	tracer.invalidate_scene();
+	tracer.trace_frame();
+	write_frame(out_prefix + '.2', { update: tracer.last_update });
+}
 tracer.close();
 console.log('trace ok: ' + JSON.stringify(tracer.last_stats));

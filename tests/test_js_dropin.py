@@ -89,3 +89,29 @@ def test_dropin_frame_equals_oracle(tmp_path, name, wh, refmax):
     assert np.array_equal(status, ref["status"])
     stats = json.loads((tmp_path / "out.json").read_text())["stats"]
     assert stats["segments"] == ref["counters"]["segments"]
+
+
+@pytest.mark.gpu
+def test_dropin_scene_edit_updates_incrementally(tmp_path):
+    """invalidate_scene() after editing the live scene: the second frame comes from rt_update_scene
+    (stable ids from serialize_scene(prev)) and equals the oracle after the same edits."""
+    spec = scenes.config1_spheres()
+    cam, cfg = scenes.make_camera(160, 120), scenes.make_config(3)
+    path = _dump(tmp_path, spec, cam, cfg)
+    A, B, Cc = 0, 3, 1                      # move sphere 0; entity 3 takes entity 1's (mirror) material
+    _node([RUNNER, path, str(tmp_path / "out"), "--edit", str(A), str(B), str(Cc)])
+    w, root = oracle.build_scene(spec)
+    e = spec.entities
+    w.move_entity(root, A, (0.5, 0.5, 0.8), e[A]["max_in_depth"], e[A]["max_out_depth"])
+    w.set_shade(B, e[Cc]["shade"], e[B]["substance"])
+    ref = w.trace_frame(root, cam, cfg, nthreads=8)
+    o = str(tmp_path / "out.2")
+    rgb = np.fromfile(o + ".rgb", dtype=np.float32)
+    assert np.array_equal(rgb.view(np.uint32), ref["rgb"].view(np.uint32))
+    assert np.array_equal(np.fromfile(o + ".ent", dtype=np.int32), ref["hit_entity"])
+    assert np.array_equal(np.fromfile(o + ".node", dtype=np.int32), ref["hit_node"])
+    assert np.array_equal(np.fromfile(o + ".status", dtype=np.uint8), ref["status"])
+    upd = json.loads((tmp_path / "out.2.json").read_text())["update"]
+    assert upd["full"] == 0 and 1 <= upd["dirty_nodes"] <= 4, upd
+    first = np.fromfile(tmp_path / "out.rgb", dtype=np.float32)
+    assert not np.array_equal(first, rgb)
