@@ -10,13 +10,21 @@ int rt_set_error(int code, const char *fmt, ...);
 
 // ---- device scene layout (HBM) ---------------------------------------------------------------
 // Node records are split by access pattern (SoA of small records):
-//   node_ps   double4  {pos.x, pos.y, pos.z, size}       read by update_next_pos / step_in
-//   node_child int32[8]                                  read on every walker slot visit
+//   node      RtNode   {pos.x, pos.y, pos.z, size, child[8]}   read by update_next_pos / step_in /
+//                                                            every walker slot visit
 //   node_up   int2     {parent, index_within_parent}     read by step_back
 //   node_ent  int2     {list begin, count}               read when a node is returned
 // Primitives are re-packed in list order (each entity appears in exactly one EntitySet), so a
 // node's entity scan streams one contiguous run of 80-byte records.
 enum : int { RT_OCT_UNDEF = -1, RT_OCT_BAD = 1000 };
+
+// A node's cube and its children in one 64-byte record: a step-in reads the child's cube, and the
+// next slot visit its child ids, from the same cache line.
+struct alignas(64) RtNode {
+    double x, y, z, s;      // OctreeDim.pos, size
+    int32_t child[8];       // child slot per octant, -1 = empty
+};
+static_assert(sizeof(RtNode) == 64, "RtNode must stay 64 bytes");
 
 struct alignas(16) RtPrim {
     double g[9];       // SPHERE: pos.xyz, dot_pp, radius_sq, within_rsq, 2/diameter
@@ -41,8 +49,7 @@ static_assert(sizeof(RtBvh) == 32, "RtBvh must stay 32 bytes");
 // Nodes live in stable slots (rt_scene.hip): slot 0 is the root; after incremental updates slot
 // order is no longer DFS order, node_dfs maps back.
 struct RtDevScene {
-    const double *node_ps;      // [n_nodes*4]
-    const int32_t *node_child;  // [n_nodes*8]
+    const RtNode *node;         // [n_nodes] cube + children, one 64-B record
     const int32_t *node_up;     // [n_nodes*2]
     const int32_t *node_ent;    // [n_nodes*4] {prim begin, count, bvh root (-1: none), 0}
     const RtPrim *prim;         // [n_list] per node in cull-hierarchy leaf order

@@ -29,7 +29,7 @@ struct NodeDims { double x, y, z, s; };
 
 __device__ __forceinline__ NodeDims node_dims(const RtDevScene &S, int n)
 {
-    const double4 v = reinterpret_cast<const double4 *>(S.node_ps)[n];
+    const double4 v = *reinterpret_cast<const double4 *>(&S.node[n].x);
     return {v.x, v.y, v.z, v.w};
 }
 
@@ -92,7 +92,7 @@ __device__ int node_at_pos(const RtDevScene &S, const double p[3], int &tree, in
         const double di = octant_sum(ix, iy, iz);
         if (!(di >= 0 && di <= 7)) return -1;
         idx = (int)di;
-        next = S.node_child[8 * cur + idx];
+        next = S.node[cur].child[idx];
         ns /= 2;
         np0 += (double)ix * ns;
         np1 += (double)iy * ns;
@@ -260,7 +260,7 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
 }
 
 // update_next_pos — :369-384 with dim_relative_to_parent :127-136.  Returns 0 or -1 (throw).
-// `p` = node_ps of w.cur_tree.
+// `p` = the cube of w.cur_tree.
 __device__ __forceinline__ int walker_update_next_pos(const NodeDims &p, Walker &w, Counters &c)
 {
     c.slot++;
@@ -297,7 +297,7 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
         int lnode;
         if (loct != RT_OCT_UNDEF) {
             if ((unsigned)loct > 7u) return -1;              // Octree.get: index out of range
-            lnode = S.node_child[8 * ltree + loct];
+            lnode = S.node[ltree].child[loct];
         } else {
             lnode = ltree;
         }
@@ -825,7 +825,7 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
             long long dummy = 0;
             if (STATS && (diag & 2)) {
                 // diag bit 1 (stats only): n_cull counts box tests of octree levels 0-1, n_exact of 2-3
-                const double lvl = log2(S.node_ps[0 * 4 + 3] / S.node_ps[4 * node + 3]);
+                const double lvl = log2(S.node[0].s / S.node[node].s);
                 box_ctr = lvl < 1.5 ? &c.cull : (lvl < 3.5 ? &c.exact : &dummy);
             }
             const long long tt0 = (STATS && (diag & 8)) ? (long long)clock64() : 0;

@@ -1,7 +1,7 @@
 // rt_scene.hip — the resident scene behind rt_upload_scene / rt_update_scene.
 //
 // Device layout (RtDevScene, rt_internal.h), in stable slots:
-//   node slots   node_ps / node_child / node_up / node_ent / node_dfs.  A full upload numbers the
+//   node slots   node (cube + children) / node_up / node_ent / node_dfs.  A full upload numbers the
 //                slots in DFS pre-order; an update keeps every existing node in its slot and
 //                appends new ones, and node_dfs maps a slot to the DFS id the outputs report.
 //   list pool    prim / list_entity / list_prefix.  A node owns a region [lbeg, lbeg+lcap) holding
@@ -41,7 +41,7 @@ int rt_build_node_cull(const RtPrim *recs, int c, int prim_base, int bvh_base, d
 
 namespace {
 
-enum Arr { A_NODE_PS, A_NODE_CHILD, A_NODE_UP, A_NODE_ENT, A_NODE_DFS, A_PRIM, A_BVH, A_LIST, A_PREFIX,
+enum Arr { A_NODE, A_NODE_UP, A_NODE_ENT, A_NODE_DFS, A_PRIM, A_BVH, A_LIST, A_PREFIX,
            A_SHADES, A_ENT_SUB, A_SUB_RI, A_N };
 
 struct DevArr {
@@ -235,8 +235,8 @@ struct RtSceneStore {
     std::vector<Slot> slots;
     std::unordered_map<Key, int32_t, KeyHash> slot_of;
     // host mirrors of the device arrays (the diff base)
-    std::vector<double> m_ps;                          // 4 / slot
-    std::vector<int32_t> m_child, m_up, m_ent, m_dfs;  // 8, 2, 4, 1 / slot
+    std::vector<RtNode> m_node;                        // 1 / slot
+    std::vector<int32_t> m_up, m_ent, m_dfs;           // 2, 4, 1 / slot
     std::vector<int32_t> m_order;                      // slot of each DFS id
     std::vector<int32_t> m_list;                       // 1 / list-pool entry
     std::vector<int32_t> m_type, m_shade, m_sub;       // 1 / entity
@@ -336,7 +336,7 @@ struct RtSceneStore {
     // Device capacities for the current high-water marks, keeping what is resident.
     int reserve_all(size_t n_slots, size_t n_ent, size_t n_shades, size_t n_ri, hipStream_t st, bool keep)
     {
-        const size_t need[A_N] = {32 * n_slots, 32 * n_slots, 8 * n_slots, 16 * n_slots, 4 * n_slots,
+        const size_t need[A_N] = {sizeof(RtNode) * n_slots, 8 * n_slots, 16 * n_slots, 4 * n_slots,
                                   sizeof(RtPrim) * list_used, sizeof(RtBvh) * bvh_used, 4 * list_used,
                                   16 * list_used, sizeof(rt_shade) * n_shades, 4 * n_ent, 8 * n_ri};
         for (int k = 0; k < A_N; k++) {
@@ -348,8 +348,7 @@ struct RtSceneStore {
 
     void fill(const rt_scene_desc *s, RtDevScene &d) const
     {
-        d.node_ps = (const double *)a[A_NODE_PS].p;
-        d.node_child = (const int32_t *)a[A_NODE_CHILD].p;
+        d.node = (const RtNode *)a[A_NODE].p;
         d.node_up = (const int32_t *)a[A_NODE_UP].p;
         d.node_ent = (const int32_t *)a[A_NODE_ENT].p;
         d.node_dfs = (const int32_t *)a[A_NODE_DFS].p;
@@ -390,8 +389,7 @@ struct RtSceneStore {
         slots.assign(N, Slot{});
         slot_of.clear();
         slot_of.reserve((size_t)N * 2);
-        m_ps.assign(4 * (size_t)N, 0);
-        m_child.assign(s->node_child, s->node_child + 8 * (size_t)N);
+        m_node.resize(N);
         m_up.assign(2 * (size_t)N, 0);
         m_ent.assign(4 * (size_t)N, 0);
         m_dfs.resize(N);
@@ -404,8 +402,10 @@ struct RtSceneStore {
         std::vector<int32_t> prefix(4 * (size_t)std::max(NL, 1));
         size_t lb = 0, bb = 0;
         for (int n = 0; n < N; n++) {
-            for (int i = 0; i < 3; i++) m_ps[4 * n + i] = s->node_pos[3 * n + i];
-            m_ps[4 * n + 3] = s->node_size[n];
+            RtNode &nd = m_node[n];
+            nd.x = s->node_pos[3 * n]; nd.y = s->node_pos[3 * n + 1]; nd.z = s->node_pos[3 * n + 2];
+            nd.s = s->node_size[n];
+            for (int k = 0; k < 8; k++) nd.child[k] = s->node_child[8 * (size_t)n + k];
             m_up[2 * n] = n == 0 ? -1 : s->node_parent[n];
             m_up[2 * n + 1] = oct[n];
             m_dfs[n] = n;
@@ -434,9 +434,9 @@ struct RtSceneStore {
         us.host_ms = ms_since(t0);
         int r = reserve_all(N, s->n_entities, s->n_shades, s->n_substances, st, false);
         if (r != RT_OK) return r;
-        const void *src[A_N] = {m_ps.data(), m_child.data(), m_up.data(), m_ent.data(), m_dfs.data(), prim.data(),
+        const void *src[A_N] = {m_node.data(), m_up.data(), m_ent.data(), m_dfs.data(), prim.data(),
                                 bvh.data(), m_list.data(), prefix.data(), s->shades, s->ent_substance, s->substance_ri};
-        const size_t bytes[A_N] = {32 * (size_t)N, 32 * (size_t)N, 8 * (size_t)N, 16 * (size_t)N, 4 * (size_t)N,
+        const size_t bytes[A_N] = {sizeof(RtNode) * (size_t)N, 8 * (size_t)N, 16 * (size_t)N, 4 * (size_t)N,
                                    sizeof(RtPrim) * lb, sizeof(RtBvh) * bb, 4 * lb, 16 * lb,
                                    sizeof(rt_shade) * (size_t)s->n_shades, 4 * (size_t)s->n_entities,
                                    8 * (size_t)s->n_substances};
@@ -468,8 +468,8 @@ struct RtSceneStore {
         for (int n = 0; n < N; n++) {
             if (i < n_old) {
                 const int32_t sl = m_order[i];
-                if (memcmp(&m_ps[4 * (size_t)sl], s->node_pos + 3 * (size_t)n, 24) == 0 &&
-                    memcmp(&m_ps[4 * (size_t)sl + 3], s->node_size + n, 8) == 0) {
+                if (memcmp(&m_node[sl].x, s->node_pos + 3 * (size_t)n, 24) == 0 &&
+                    memcmp(&m_node[sl].s, s->node_size + n, 8) == 0) {
                     slot_of_dfs[n] = sl;
                     i++;
                     continue;
@@ -570,8 +570,7 @@ struct RtSceneStore {
         // node records: new slots, and the existing parents that gained a child (an existing node's
         // cube, parent and octant never change); node_dfs wherever the DFS numbering shifted
         std::vector<int32_t> touched;                 // slots whose ps / child / up records are rewritten
-        m_ps.resize(4 * n_slots);
-        m_child.resize(8 * n_slots);
+        m_node.resize(n_slots);
         m_up.resize(2 * n_slots);
         std::vector<int32_t> n_dfs(m_dfs);
         n_dfs.resize(n_slots);
@@ -582,8 +581,9 @@ struct RtSceneStore {
             m_order[n] = sl;
             if (sl < (int)n_old) continue;
             touched.push_back(sl);
-            for (int k = 0; k < 3; k++) m_ps[4 * (size_t)sl + k] = s->node_pos[3 * (size_t)n + k];
-            m_ps[4 * (size_t)sl + 3] = s->node_size[n];
+            RtNode &nd = m_node[sl];
+            nd.x = s->node_pos[3 * (size_t)n]; nd.y = s->node_pos[3 * (size_t)n + 1]; nd.z = s->node_pos[3 * (size_t)n + 2];
+            nd.s = s->node_size[n];
             m_up[2 * (size_t)sl] = n == 0 ? -1 : slot_of_dfs[s->node_parent[n]];
             m_up[2 * (size_t)sl + 1] = oct[n];
             if (n > 0 && slot_of_dfs[s->node_parent[n]] < (int)n_old) touched.push_back(slot_of_dfs[s->node_parent[n]]);
@@ -597,11 +597,10 @@ struct RtSceneStore {
             const int n = dfs_of_slot[sl];
             for (int k = 0; k < 8; k++) {
                 const int ch = s->node_child[8 * (size_t)n + k];
-                m_child[8 * (size_t)sl + k] = ch < 0 ? -1 : slot_of_dfs[ch];
+                m_node[sl].child[k] = ch < 0 ? -1 : slot_of_dfs[ch];
             }
         }
-        add_slots(A_NODE_PS, touched, m_ps.data(), 4 * sizeof(double));
-        add_slots(A_NODE_CHILD, touched, m_child.data(), 8 * sizeof(int32_t));
+        add_slots(A_NODE, touched, m_node.data(), sizeof(RtNode));
         add_slots(A_NODE_UP, touched, m_up.data(), 2 * sizeof(int32_t));
         diff_runs(A_NODE_DFS, n_dfs, m_dfs, 1);
         std::vector<int32_t> ent_slots;

@@ -58,6 +58,9 @@ class StripeGather:
             self._src = torch.from_numpy(src).to(device)
         else:
             self._bufs, self._src = None, None
+        if self.local.is_cuda:
+            # the fills ran on torch's stream; rt_trace_rows_device writes `local` on another one
+            torch.cuda.synchronize(self.local.device)
 
     def gather(self):
         """Collective (every rank calls it): rank 0's `frame` receives the whole image."""

@@ -93,10 +93,12 @@ def test_device_stats_and_tonemap_goldens(gold):
         for c in gold:
             n = c["n_pixels"]
             d = torch.from_numpy(c["rgb"]).cuda()
+            torch.cuda.synchronize()
             st = ctx.exposure_stats_device(d.data_ptr(), n)
             _stats_close([st.mean, st.variance, st.absdev], c["stats"], n)
             for key, (lo, hi) in (("rgba_stddev", c["ranges"][1]), ("rgba_identity", (0.0, 1.0))):
                 out = torch.zeros(4 * n, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()            # the fill runs on torch's stream, the kernel on the context's
                 ctx.tonemap_device(d.data_ptr(), n, lo, hi, out.data_ptr())
                 torch.cuda.synchronize()
                 assert np.array_equal(out.cpu().numpy(), np.array(c[key], np.uint8)), (c["name"], key)
@@ -119,6 +121,7 @@ def test_progressive_exposure_device_resident():
         ctx.upload(rtamd.build_scene(spec))
         buf = torch.full((H, W, 3), 123.0, dtype=torch.float32, device="cuda")
         s = torch.cuda.Stream()
+        torch.cuda.synchronize()
         for k, cam in enumerate(cams):
             cfg = scenes.make_config(3, col_weight=1 / (1 + k))
             w.trace_frame(root, cam, cfg, rgb=ref, nthreads=4)
@@ -131,6 +134,7 @@ def test_progressive_exposure_device_resident():
         _stats_close([st.mean, st.variance, st.absdev], ref_st, W * H)
         lo, hi = oracle.tonemap_range(1, ref_st)
         out = torch.zeros(4 * W * H, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()                    # the fill runs on torch's stream, the kernel on `s`
         ctx.tonemap_device(buf.data_ptr(), W * H, lo, hi, out.data_ptr(), s.cuda_stream)
         s.synchronize()
         assert np.array_equal(out.cpu().numpy(), oracle.tonemap(ref, lo, hi))
@@ -151,6 +155,7 @@ def test_stats_full_hd_frame():
         ctx.upload(rtamd.build_scene(spec))
         buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
         s = torch.cuda.Stream()
+        torch.cuda.synchronize()
         ctx.trace_rows_device(cam, cfg, 0, 1, 8, buf.data_ptr(), s.cuda_stream)
         st = ctx.exposure_stats_device(buf.data_ptr(), W * H, s.cuda_stream)
         host = buf.reshape(-1).cpu().numpy()
@@ -158,6 +163,7 @@ def test_stats_full_hd_frame():
         _stats_close([st.mean, st.variance, st.absdev], ref_st, W * H)
         lo, hi = oracle.tonemap_range(1, ref_st)
         out = torch.zeros(4 * W * H, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
         ctx.tonemap_device(buf.data_ptr(), W * H, lo, hi, out.data_ptr(), s.cuda_stream)
         s.synchronize()
         assert np.array_equal(out.cpu().numpy(), oracle.tonemap(host, lo, hi))

@@ -214,6 +214,7 @@ def test_rough_parts_reassemble(n, stripe):
         ctx.trace_rows_device(cam, cfg, 0, 1, stripe, full.local.data_ptr(), s.cuda_stream)
         src, max_rows = source_index(H, n, stripe)
         stacked = torch.full((n * max_rows, W, 3), float("nan"), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()                    # the fills run on torch's stream, the frames on `s`
         for p in range(n):
             rows, _ = ctx.trace_rows_device(cam, cfg, p, n, stripe, stacked[p * max_rows].data_ptr(), s.cuda_stream)
             assert rows == len(part_rows(H, p, n, stripe))

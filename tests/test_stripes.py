@@ -107,6 +107,7 @@ def test_parts_reassemble_to_full_frame_gpu(n, stripe):
         assert rows == H
         src, max_rows = source_index(H, n, stripe)
         stacked = torch.full((n * max_rows, W, 3), float("nan"), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()                    # the fills run on torch's stream, the frames on `s`
         for p in range(n):
             rows, _ = ctx.trace_rows_device(cam, cfg, p, n, stripe, stacked[p * max_rows].data_ptr(), s.cuda_stream)
             assert rows == len(part_rows(H, p, n, stripe))
