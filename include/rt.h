@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2   /* 2: rt_config_desc gained scatter_seed / scatter_mode */
+#define RT_ABI_VERSION 3   /* 2: rt_config_desc gained scatter_seed / scatter_mode;
+                              3: image textures (rt_image_desc, rt_shade.image, sky_image) */
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define RT_OK             0
@@ -56,16 +57,28 @@ extern "C" {
 #define RT_RESP_TRANSMISSION 1
 #define RT_RESP_BOTH         2
 
-/* One (Material, SolidTexture) pair as seen by an entity: StaticMaterial fields
- * (src/material.ts:67-103) + the texture's solid colour (src/texture/texture_solid.ts:33-35). */
+/* One (Material, Texture) pair as seen by an entity: StaticMaterial fields
+ * (src/material.ts:67-103) + the texture: a SolidTexture colour (src/texture/texture_solid.ts:33-35)
+ * or a loaded ImageTexture (src/texture/texture_image.ts:40-63). */
 typedef struct rt_shade {
     int32_t response;    /* RT_RESP_*                                */
     int32_t light;       /* StaticMaterial.light_source              */
     int32_t mirror;      /* StaticMaterial.mirror                    */
-    int32_t pad_;
-    double  roughness;   /* StaticMaterial.roughness_index (must be 0 for rt_trace_*; see RT_E_UNSUPPORTED) */
+    int32_t image;       /* 0: SolidTexture `rgb`; k >= 1: ImageTexture rt_scene_desc.images[k-1],
+                            looked up at entity.map_uv(point) (sphere: uv_map_sphere(p - pos),
+                            src/entities/entity_sphere.ts:98-101; box and face: (0, 0)) */
+    double  roughness;   /* StaticMaterial.roughness_index (> 0 on a mirror: see RT_SCATTER_*) */
     double  rgb[3];      /* SolidTexture colour (alpha is never read on the path) */
 } rt_shade;
+
+/* A loaded ImageTexture: image_data (src/texture/texture_image.ts:75-124) is the canvas's bytes
+ * divided by 255.0 after the optional flips, W*H*3 values row by row; the bytes are carried and
+ * divided on the device, which yields the identical doubles.  get_color(u, v) reads texel
+ * ((v*height) << 0) * width + ((u*width) << 0) and throws outside [-eps, 1-eps]. */
+typedef struct rt_image_desc {
+    int32_t width, height;
+    const uint8_t *rgb;           /* [height*width*3]                                          */
+} rt_image_desc;
 
 /* Per-entity geometry, 9 doubles (ent_geom[9*i .. 9*i+8]):
  *   SPHERE: pos.xyz, diameter, sphere_math._dot_pp, sphere_math._radius_sq, entity._radius_sq, 0, 0
@@ -82,7 +95,7 @@ typedef struct rt_scene_desc {
     int32_t n_entities;
     int32_t n_shades;
     int32_t n_substances;
-    int32_t pad_;
+    int32_t n_images;             /* ImageTextures referenced by rt_shade.image / sky_image   */
     const double  *node_pos;      /* [n_nodes*3]  OctreeDim.pos                                */
     const double  *node_size;     /* [n_nodes]    OctreeDim.size                               */
     const int32_t *node_parent;   /* [n_nodes]    -1 for the root                              */
@@ -96,6 +109,7 @@ typedef struct rt_scene_desc {
     const int32_t *ent_substance; /* [n_entities] index into substance_ri, -1 = undefined      */
     const rt_shade *shades;       /* [n_shades]                                                */
     const double  *substance_ri;  /* [n_substances] Substance.refractive_index (src/substance.ts) */
+    const rt_image_desc *images;  /* [n_images]                                                */
 } rt_scene_desc;
 
 /* ---- per-frame inputs -------------------------------------------------------------------- */
@@ -125,7 +139,9 @@ typedef struct rt_config_desc {
     double  col_weight;                 /* 1.0 after reset_exposure()              */
     uint64_t scatter_seed;              /* RT_SCATTER_COUNTER: key of this frame's draws          */
     int32_t scatter_mode;               /* RT_SCATTER_*                                           */
-    int32_t pad_;
+    int32_t sky_image;                  /* 0: SkySphere(SolidTexture(sky_rgb)); k >= 1: SkySphere of
+                                           ImageTexture images[k-1] at uv_map_sphere(dir)
+                                           (src/sky/sky_sphere.ts:23-26)                         */
 } rt_config_desc;
 
 /* Rough mirrors (roughness_index > 0): scatter_ray (src/raytracer.ts:121-133) draws from the

@@ -63,6 +63,11 @@ def lib():
     L.orc_tonemap_range.argtypes = [i, pd, i, C.c_double, C.c_double, pd]
     L.orc_tonemap.argtypes = [pf, C.c_int64, C.c_double, C.c_double, C.POINTER(C.c_uint8)]
     L.orc_tonemap.restype = None
+    L.orc_set_images.argtypes = [vp, C.POINTER(abi.rt_image_desc), i]
+    L.orc_atan2.argtypes = [C.c_double, C.c_double]
+    L.orc_atan2.restype = C.c_double
+    L.orc_uv_map_sphere.argtypes = [pd, pd]
+    L.orc_uv_map_sphere.restype = None
     L.orc_move_entity.argtypes = [vp, vp, i, pd, i, i]
     L.orc_set_shade.argtypes = [vp, i, i, i]
     L.orc_counter_draw_at.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
@@ -168,6 +173,15 @@ class World:
         self.L.orc_set_tables(self.h, shades.ctypes.data_as(C.POINTER(abi.rt_shade)), len(shades),
                               ri.ctypes.data_as(C.POINTER(C.c_double)), len(ri))
 
+    def set_images(self, images):
+        """ImageTextures, [H, W, 3] uint8 each (copied by the oracle)."""
+        imgs = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+        arr = (abi.rt_image_desc * max(1, len(imgs)))()
+        for k, im in enumerate(imgs):
+            arr[k].height, arr[k].width = im.shape[0], im.shape[1]
+            arr[k].rgb = im.ctypes.data_as(C.POINTER(C.c_uint8))
+        self.L.orc_set_images(self.h, arr, len(imgs))
+
     def add_entity(self, tree, etype, geom, shade=0, substance=-1, max_in_depth=10, max_out_depth=0):
         g = (C.c_double * 9)(*([float(x) for x in geom] + [0.0] * (9 - len(geom))))
         fit = C.c_void_p()
@@ -263,8 +277,20 @@ def build_scene(spec):
     w = World()
     root = w.tree(spec.root_pos, spec.root_size, True)
     w.set_tables(spec.shades, spec.substances)
+    w.set_images(spec.images)
     w.add_entities(root, spec.entities)
     return w, root
+
+
+def atan2(y, x):
+    """Math.atan2 as V8 computes it (fdlibm)."""
+    return lib().orc_atan2(float(y), float(x))
+
+
+def uv_map_sphere(d):
+    uv = np.zeros(2)
+    lib().orc_uv_map_sphere(_vec(d), uv.ctypes.data_as(C.POINTER(C.c_double)))
+    return uv
 
 
 # ---- ExposureBuffer consumers (src/view/exposure_buffer.ts, src/view/tone_mapping.ts) ----------------

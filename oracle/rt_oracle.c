@@ -113,6 +113,8 @@ struct oworld {
     int n_shades;
     double *ri;
     int n_ri;
+    rt_image_desc *images;   /* ImageTextures (each rgb a private copy) */
+    int n_images;
 };
 
 oworld *orc_world_new(void)
@@ -128,6 +130,8 @@ void orc_world_free(oworld *w)
     free(w->ents);
     free(w->shades);
     free(w->ri);
+    for (int i = 0; i < w->n_images; i++) free((void *)w->images[i].rgb);
+    free(w->images);
     free(w);
 }
 
@@ -517,6 +521,140 @@ int orc_set_tables(oworld *w, const rt_shade *shades, int n_shades, const double
     if (n_ri) memcpy(w->ri, ri, sizeof(double) * (size_t)n_ri);
     w->n_shades = n_shades;
     w->n_ri = n_ri;
+    return 0;
+}
+
+/* Loaded ImageTextures (rt_image_desc: the canvas bytes behind image_data, which holds them / 255.0) */
+int orc_set_images(oworld *w, const rt_image_desc *images, int n)
+{
+    for (int i = 0; i < w->n_images; i++) free((void *)w->images[i].rgb);
+    free(w->images);
+    w->images = (rt_image_desc *)calloc((size_t)(n > 0 ? n : 1), sizeof(rt_image_desc));
+    for (int i = 0; i < n; i++) {
+        size_t b = (size_t)images[i].width * (size_t)images[i].height * 3;
+        uint8_t *px = (uint8_t *)malloc(b ? b : 1);
+        memcpy(px, images[i].rgb, b);
+        w->images[i].width = images[i].width;
+        w->images[i].height = images[i].height;
+        w->images[i].rgb = px;
+    }
+    w->n_images = n;
+    return 0;
+}
+
+/* ---- Math.atan / Math.atan2 (V8 = fdlibm s_atan.c / e_atan2.c), needed bit-exact by
+ * uv_map_sphere (src/math/uv_mapping.ts:19-25).  Pinned against node (tests/golden). */
+static uint32_t orc_hi(double x) { uint64_t b; memcpy(&b, &x, 8); return (uint32_t)(b >> 32); }
+static uint32_t orc_lo(double x) { uint64_t b; memcpy(&b, &x, 8); return (uint32_t)b; }
+
+static const double ATANHI[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
+                                 9.82793723247329054082e-01, 1.57079632679489655800e+00};
+static const double ATANLO[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,
+                                 1.39033110312309984516e-17, 6.12323399573676603587e-17};
+static const double AT[11] = {3.33333333333329318027e-01, -1.99999999998764832476e-01,
+                              1.42857142725034663711e-01, -1.11111104054623557880e-01,
+                              9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                              6.66107313738753120669e-02, -5.83357013379057348645e-02,
+                              4.97687799461593236017e-02, -3.65315727442169155270e-02,
+                              1.62858201153657823623e-02};
+
+double orc_atan(double x)
+{
+    int32_t hx = (int32_t)orc_hi(x);
+    uint32_t ix = (uint32_t)hx & 0x7fffffffu;
+    int id;
+    if (ix >= 0x44100000u) {
+        if (ix > 0x7ff00000u || (ix == 0x7ff00000u && orc_lo(x) != 0)) return x + x;
+        return hx > 0 ? ATANHI[3] + ATANLO[3] : -ATANHI[3] - ATANLO[3];
+    }
+    if (ix < 0x3fdc0000u) {
+        if (ix < 0x3e400000u) return x;
+        id = -1;
+    } else {
+        x = fabs(x);
+        if (ix < 0x3ff30000u) {
+            if (ix < 0x3fe60000u) { id = 0; x = (2.0 * x - 1.0) / (2.0 + x); }
+            else { id = 1; x = (x - 1.0) / (x + 1.0); }
+        } else if (ix < 0x40038000u) { id = 2; x = (x - 1.5) / (1.0 + 1.5 * x); }
+        else { id = 3; x = -1.0 / x; }
+    }
+    double z = x * x, w = z * z;
+    double s1 = z * (AT[0] + w * (AT[2] + w * (AT[4] + w * (AT[6] + w * (AT[8] + w * AT[10])))));
+    double s2 = w * (AT[1] + w * (AT[3] + w * (AT[5] + w * (AT[7] + w * AT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    z = ATANHI[id] - ((x * (s1 + s2) - ATANLO[id]) - x);
+    return hx < 0 ? -z : z;
+}
+
+double orc_atan2(double y, double x)
+{
+    const double tiny = 1.0e-300, pi_o_4 = 7.8539816339744827900e-01, pi_o_2 = 1.5707963267948965580e+00;
+    const double pi = 3.1415926535897931160e+00, pi_lo = 1.2246467991473531772e-16;
+    int32_t hx = (int32_t)orc_hi(x), hy = (int32_t)orc_hi(y);
+    uint32_t ix = (uint32_t)hx & 0x7fffffffu, iy = (uint32_t)hy & 0x7fffffffu;
+    uint32_t lx = orc_lo(x), ly = orc_lo(y);
+    if ((ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000u || (iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000u) return x + y;
+    if ((((uint32_t)hx - 0x3ff00000u) | lx) == 0) return orc_atan(y);
+    int m = (int)(((uint32_t)hy >> 31) & 1u) | (int)(((uint32_t)hx >> 30) & 2u);
+    if ((iy | ly) == 0) {
+        if (m < 2) return y;
+        return m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if ((ix | lx) == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7ff00000u) {
+        if (iy == 0x7ff00000u) {
+            if (m == 0) return pi_o_4 + tiny;
+            if (m == 1) return -pi_o_4 - tiny;
+            if (m == 2) return 3.0 * pi_o_4 + tiny;
+            return -3.0 * pi_o_4 - tiny;
+        }
+        if (m == 0) return 0.0;
+        if (m == 1) return -0.0;
+        if (m == 2) return pi + tiny;
+        return -pi - tiny;
+    }
+    if (iy == 0x7ff00000u) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    int k = ((int32_t)iy - (int32_t)ix) >> 20;
+    double z;
+    if (k > 60) { z = pi_o_2 + 0.5 * pi_lo; m &= 1; }
+    else if (hx < 0 && k < -60) z = 0.0;
+    else z = orc_atan(fabs(y / x));
+    if (m == 0) return z;
+    if (m == 1) return -z;
+    if (m == 2) return pi - (z - pi_lo);
+    return (z - pi_lo) - pi;
+}
+
+/* uv_map_sphere (src/math/uv_mapping.ts:19-25) */
+void orc_uv_map_sphere(const double d[3], double uv[2])
+{
+    const double PI = 3.141592653589793, EPS = 2.220446049250313e-16;
+    uv[0] = orc_atan2(d[1], d[0]) / PI / 2.0 + 0.5 - EPS;
+    double len = sqrt((0.0 + d[0] * d[0]) + d[1] * d[1]);     /* vector.length(vector.reduce(dir, 2)) */
+    uv[1] = orc_atan2(d[2], len) / PI + 0.5 - EPS;
+}
+
+/* ToInt32 of a finite double below 2^31 in magnitude (u*width, v*height): truncation */
+static int32_t orc_toint32_small(double x)
+{
+    if (!(fabs(x) < 2147483648.0)) {
+        if (!isfinite(x)) return 0;
+        double m = fmod(trunc(x), 4294967296.0);
+        if (m < 0) m += 4294967296.0;
+        return (int32_t)(uint32_t)m;
+    }
+    return (int32_t)x;
+}
+
+/* ImageTexture.get_color (src/texture/texture_image.ts:40-63) of image k (1-based): 0 ok, -1 throw */
+static int orc_image_color(const oworld *w, int k, double u, double v, double rgb[3])
+{
+    const double EPS = 2.220446049250313e-16;
+    const rt_image_desc *im = &w->images[k - 1];
+    if (u < 0 - EPS || u > 1 - EPS || v < 0 - EPS || v > 1 - EPS) return -1;  /* 'Texture coordinates out of bounds' */
+    int32_t ui = orc_toint32_small(u * im->width), vi = orc_toint32_small(v * im->height);
+    int64_t px_idx = ((int64_t)vi * im->width + ui) * 3;
+    for (int c = 0; c < 3; c++) rgb[c] = (double)im->rgb[px_idx + c] / 255.0;   /* image_data[i] = byte / 255.0 */
     return 0;
 }
 
@@ -1112,7 +1250,20 @@ static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], ui
         const oentity *e = &w->ents[hit_id];
         const rt_shade *sh = &w->shades[e->shade];
         /* SolidMaterial.alter_ray → mul_color (src/materials/material_solid.ts:30-36, src/physics/color.ts:50-52) */
-        for (int i = 0; i < 3; i++) col[i] = col[i] * sh->rgb[i];
+        if (sh->image) {
+            /* texture.get_color(entity.map_uv(point)): sphere uv_map_sphere(vector.sub(p, pos))
+             * (src/entities/entity_sphere.ts:98-101); box (src/entities/entity_box.ts:104-107) and
+             * face: [0, 0] */
+            double uv[2] = {0, 0}, tc[3];
+            if (e->type == RT_ENT_SPHERE) {
+                double dist[3] = {h.point[0] - e->g[0], h.point[1] - e->g[1], h.point[2] - e->g[2]};
+                orc_uv_map_sphere(dist, uv);
+            }
+            if (orc_image_color(w, sh->image, uv[0], uv[1], tc) < 0) { ro->status = ST_FAULT; goto out; }
+            for (int i = 0; i < 3; i++) col[i] = col[i] * tc[i];
+        } else {
+            for (int i = 0; i < 3; i++) col[i] = col[i] * sh->rgb[i];
+        }
         double diff[3] = {h.point[0] - o[0], h.point[1] - o[1], h.point[2] - o[2]};
         path += sqrt(vdot(diff, diff));
         o[0] = h.point[0]; o[1] = h.point[1]; o[2] = h.point[2];
@@ -1163,7 +1314,15 @@ static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], ui
         ro->segments++;
     }
     if (!light_hit) {
-        for (int i = 0; i < 3; i++) col[i] = col[i] * cfg->sky_rgb[i];   /* sky.get_color(dir) */
+        if (cfg->sky_image) {
+            /* SkySphere.get_color(this.dir) — src/sky/sky_sphere.ts:23-26 */
+            double uv[2], tc[3];
+            orc_uv_map_sphere(d, uv);
+            if (orc_image_color(w, cfg->sky_image, uv[0], uv[1], tc) < 0) { ro->status = ST_FAULT; goto out; }
+            for (int i = 0; i < 3; i++) col[i] = col[i] * tc[i];
+        } else {
+            for (int i = 0; i < 3; i++) col[i] = col[i] * cfg->sky_rgb[i];   /* sky.get_color(dir) */
+        }
     } else {
         double t = path * cfg->distance_attenuation_factor;
         double isl = 1.0 / (2.220446049250313e-16 + t * t);   /* (x)**2 == x*x (fdlibm pow special case) */

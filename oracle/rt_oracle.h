@@ -57,6 +57,10 @@ int      orc_walker_next(owalker *wk, onode **node, onode **pos_tree, int *pos_o
 
 /* --- scene (src/octree_entity.ts, src/entity.ts, src/entities/) --- */
 int  orc_set_tables(oworld *w, const rt_shade *shades, int n_shades, const double *ri, int n_ri);
+int  orc_set_images(oworld *w, const rt_image_desc *images, int n);      /* ImageTextures (copied) */
+double orc_atan(double x);                                                 /* Math.atan (V8 / fdlibm) */
+double orc_atan2(double y, double x);                                      /* Math.atan2 (V8 / fdlibm) */
+void orc_uv_map_sphere(const double d[3], double uv[2]);                  /* src/math/uv_mapping.ts:19-25 */
 /* add_entity_to_octree(tree, entity, {max_in_depth, max_out_depth}) (:174-188); returns entity id
  * (creation order) or <0; *fitting receives the node holding the entity. */
 int  orc_add_entity(oworld *w, onode *tree, int type, const double geom[9], int shade, int substance,

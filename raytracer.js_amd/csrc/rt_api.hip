@@ -71,6 +71,7 @@ struct rt_ctx {
     bool bvh_sah = true;             // SAH splits (RT_BVH_SAH=0: median split)
     bool split = true;               // walk pass + test pass (RT_SPLIT=0: fused k_trace)
     int cand_cap = 64;               // candidate nodes per pixel in the split path (RT_CAND_CAP)
+    int split_levels = RT_MAX_LEVELS + 1;   // split-path bounce levels (RT_SPLIT_LEVELS)
     int cont_group = 8;              // continuation rays per wave (RT_CONT_GROUP): their passes are
                                      // latency-bound, fewer lanes per wave shorten the slowest wave
     int occ = 0;
@@ -111,6 +112,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_SPLIT")) c->split = atoi(e) != 0;
     if (c->flags & RT_CREATE_NO_SPLIT) c->split = false;
     if (const char *e = getenv("RT_CAND_CAP")) c->cand_cap = atoi(e) < 1 ? 1 : atoi(e);
+    if (const char *e = getenv("RT_SPLIT_LEVELS")) c->split_levels = atoi(e) < 1 ? 1 : atoi(e);
     if (const char *e = getenv("RT_CONT_GROUP")) c->cont_group = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
@@ -181,6 +183,8 @@ static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_confi
         return rt_set_error(RT_E_INVALID, "bad screen size %dx%d", cam->width, cam->height);
     if (cfg->default_substance < -1 || cfg->default_substance >= c->scene.n_subs)
         return rt_set_error(RT_E_INVALID, "bad default_substance %d", cfg->default_substance);
+    if (cfg->sky_image < 0 || cfg->sky_image > c->scene.n_images)
+        return rt_set_error(RT_E_INVALID, "bad sky_image %d (%d images)", cfg->sky_image, c->scene.n_images);
     if (cfg->scatter_mode != RT_SCATTER_REJECT && cfg->scatter_mode != RT_SCATTER_COUNTER)
         return rt_set_error(RT_E_INVALID, "bad scatter_mode %d", cfg->scatter_mode);
     if (c->scatter && cfg->scatter_mode != RT_SCATTER_COUNTER)
@@ -225,6 +229,7 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.occ = c->occ;
     L.diag = c->diag;
     L.cont_group = c->cont_group;
+    L.split_levels = c->split_levels;
     if (c->split && P > 0) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).

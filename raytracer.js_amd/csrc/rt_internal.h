@@ -26,6 +26,12 @@ struct alignas(64) RtNode {
 };
 static_assert(sizeof(RtNode) == 64, "RtNode must stay 64 bytes");
 
+// A loaded ImageTexture (rt_image_desc): width x height RGB bytes at texels + offset.
+struct RtImage {
+    int64_t offset;
+    int32_t width, height;
+};
+
 struct alignas(16) RtPrim {
     double g[9];       // SPHERE: pos.xyz, dot_pp, radius_sq, within_rsq, 2/diameter
                        // BOX:    pos.xyz, size
@@ -60,7 +66,9 @@ struct RtDevScene {
     const int32_t *ent_sub;     // [n_entities]
     const double *sub_ri;       // [n_substances]
     const int32_t *node_dfs;    // [n_nodes] DFS pre-order id of each node slot (the reported node id)
-    int32_t n_nodes, n_list, n_entities, n_shades, n_subs, n_bvh;
+    const RtImage *images;      // [n_images] ImageTextures: texel bytes at texels + offset
+    const uint8_t *texels;
+    int32_t n_nodes, n_list, n_entities, n_shades, n_subs, n_bvh, n_images;
 };
 
 // A ray of the split path at its first continuation (segment start after a mirror / transmission
@@ -120,6 +128,7 @@ struct RtLaunch {
     struct RtCont *ovf;                         // device [rows*W]: rays left to the fused kernel
     int32_t level, last_level;                  // set per launch by rt_launch_frame
     int32_t cont_group;                         // continuation rays per wave (levels >= 1)
+    int32_t split_levels;                       // bounce levels on the split path; deeper ones run in k_cont
 };
 
 enum { RT_MAX_LEVELS = 32, RT_CTR_INTS = 4 + 4 * (RT_MAX_LEVELS + 1) };

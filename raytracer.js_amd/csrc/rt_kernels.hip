@@ -13,6 +13,8 @@
 // (built with -ffp-contract=off), JS ToInt32 for `<<`.  Branchy pointer-chasing work: no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rt_internal.h"
 #include "rt_jsnum.h"
 
@@ -708,6 +710,20 @@ __device__ __forceinline__ void queue_push(RtCont *q, int32_t *qn, const double 
     e.pad[1] = (int32_t)draws;
 }
 
+// ImageTexture.get_color(u, v) (src/texture/texture_image.ts:40-63) of image k (1-based): the texel's
+// bytes / 255.0, as image_data holds them.  false where the reference throws.
+__device__ __forceinline__ bool image_color(const RtDevScene &S, int k, double u, double v, double rgb[3])
+{
+    const RtImage im = S.images[k - 1];
+    const int64_t t = texel_index(u, v, im.width, im.height);
+    if (t < 0) return false;
+    const uint8_t *px = S.texels + im.offset + 3 * t;
+    rgb[0] = (double)px[0] / 255.0;
+    rgb[1] = (double)px[1] / 255.0;
+    rgb[2] = (double)px[2] / 255.0;
+    return true;
+}
+
 // RT_SCATTER_COUNTER key: the full-frame pixel index y*W + x of part-local pixel `pix`.
 __device__ __forceinline__ uint64_t frame_pixel(const RtLaunch &L, int pix)
 {
@@ -840,7 +856,18 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         refcount++;
         c.hit++;
         const rt_shade sh = S.shades[pr.meta >> 2];
-        col0 = col0 * sh.rgb[0]; col1 = col1 * sh.rgb[1]; col2 = col2 * sh.rgb[2];      // mul_color
+        // SolidMaterial.alter_ray (src/materials/material_solid.ts:30-36): mul_color with
+        // texture.get_color(entity.map_uv(p))
+        if (sh.image) {
+            double u = 0, v = 0;                              // BoxEntity / FaceEntity map_uv: [0, 0]
+            if ((pr.meta & 3) == RT_ENT_SPHERE)               // vector.sub(p, this.pos)
+                uv_map_sphere(h.p[0] - pr.g[0], h.p[1] - pr.g[1], h.p[2] - pr.g[2], u, v);
+            double tc[3];
+            if (!image_color(S, sh.image, u, v, tc)) { R.status = ST_FAULT; goto done; }
+            col0 = col0 * tc[0]; col1 = col1 * tc[1]; col2 = col2 * tc[2];
+        } else {
+            col0 = col0 * sh.rgb[0]; col1 = col1 * sh.rgb[1]; col2 = col2 * sh.rgb[2];  // mul_color
+        }
         {
             const double a = h.p[0] - o[0], b = h.p[1] - o[1], e = h.p[2] - o[2];
             path += sqrt(dot3(a, b, e, a, b, e));
@@ -899,7 +926,15 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         seat = true;
     }
     if (!light_hit) {
-        col0 = col0 * cfg.sky_rgb[0]; col1 = col1 * cfg.sky_rgb[1]; col2 = col2 * cfg.sky_rgb[2];
+        if (cfg.sky_image) {
+            // SkySphere.get_color(this.dir) (src/sky/sky_sphere.ts:23-26)
+            double u, v, tc[3];
+            uv_map_sphere(d[0], d[1], d[2], u, v);
+            if (!image_color(S, cfg.sky_image, u, v, tc)) { R.status = ST_FAULT; goto done; }
+            col0 = col0 * tc[0]; col1 = col1 * tc[1]; col2 = col2 * tc[2];
+        } else {
+            col0 = col0 * cfg.sky_rgb[0]; col1 = col1 * cfg.sky_rgb[1]; col2 = col2 * cfg.sky_rgb[2];
+        }
     } else {
         const double t = path * cfg.distance_attenuation_factor;
         const double isl = 1.0 / (2.220446049250313e-16 + t * t);
@@ -1267,7 +1302,8 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
         // takes the primary rays by tiles, level lv >= 1 the continuations queued at lv - 1.  Rays
         // reaching refmax end inside the shading pass, so refmax - 1 levels carry all bounces.
         const long long want = (long long)L.cfg.refmax - 1;
-        const int levels = (int)(want < 0 ? 0 : (want > RT_MAX_LEVELS ? RT_MAX_LEVELS : want));
+        const long long cap = std::min<long long>(RT_MAX_LEVELS, (long long)L.split_levels - 1);
+        const int levels = (int)(want < 0 ? 0 : (want > cap ? cap : want));
         for (int lv = 0; lv <= levels; lv++) {
             RtLaunch Lv = L;
             Lv.level = lv;

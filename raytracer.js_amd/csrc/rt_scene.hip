@@ -42,7 +42,7 @@ int rt_build_node_cull(const RtPrim *recs, int c, int prim_base, int bvh_base, d
 namespace {
 
 enum Arr { A_NODE, A_NODE_UP, A_NODE_ENT, A_NODE_DFS, A_PRIM, A_BVH, A_LIST, A_PREFIX,
-           A_SHADES, A_ENT_SUB, A_SUB_RI, A_N };
+           A_SHADES, A_ENT_SUB, A_SUB_RI, A_IMAGES, A_TEXELS, A_N };
 
 struct DevArr {
     void *p = nullptr;
@@ -183,6 +183,15 @@ int validate(const rt_scene_desc *s, std::vector<int32_t> &oct, bool &scatter)
         if (s->ent_substance[e] < -1 || s->ent_substance[e] >= s->n_substances)
             return rt_set_error(RT_E_INVALID, "rt_upload_scene: entity %d substance", e);
     }
+    if (s->n_images < 0 || (s->n_images && !s->images)) return rt_set_error(RT_E_INVALID, "rt_upload_scene: images");
+    for (int i = 0; i < s->n_images; i++) {
+        const rt_image_desc &im = s->images[i];
+        if (im.width < 1 || im.height < 1 || !im.rgb || (long long)im.width * im.height > (1ll << 31) / 3)
+            return rt_set_error(RT_E_INVALID, "rt_upload_scene: image %d (%dx%d)", i, im.width, im.height);
+    }
+    for (int i = 0; i < s->n_shades; i++)
+        if (s->shades[i].image < 0 || s->shades[i].image > s->n_images)
+            return rt_set_error(RT_E_INVALID, "rt_upload_scene: shade %d image %d", i, s->shades[i].image);
     scatter = false;
     for (int k = 0; k < NL; k++) {
         const int e = s->list_entity[k];
@@ -243,6 +252,8 @@ struct RtSceneStore {
     std::vector<double> m_geom;                        // 9 / entity
     std::vector<rt_shade> m_shades;
     std::vector<double> m_ri;
+    std::vector<RtImage> m_images;
+    std::vector<uint8_t> m_texels;                     // all images' bytes, padded to 4
     size_t list_used = 0, bvh_used = 0;
     DevArr a[A_N];
     // staging
@@ -333,12 +344,29 @@ struct RtSceneStore {
         return RT_OK;
     }
 
+    // The image table and the texel pool of a desc (each image 4-byte aligned).
+    static void pack_images(const rt_scene_desc *s, std::vector<RtImage> &tab, std::vector<uint8_t> &tex)
+    {
+        tab.resize(s->n_images);
+        size_t off = 0;
+        for (int i = 0; i < s->n_images; i++) {
+            const rt_image_desc &im = s->images[i];
+            tab[i] = {(int64_t)off, im.width, im.height};
+            off += ((size_t)im.width * im.height * 3 + 3) & ~(size_t)3;
+        }
+        tex.assign(off, 0);
+        for (int i = 0; i < s->n_images; i++)
+            memcpy(&tex[tab[i].offset], s->images[i].rgb, (size_t)s->images[i].width * s->images[i].height * 3);
+    }
+
     // Device capacities for the current high-water marks, keeping what is resident.
-    int reserve_all(size_t n_slots, size_t n_ent, size_t n_shades, size_t n_ri, hipStream_t st, bool keep)
+    int reserve_all(size_t n_slots, size_t n_ent, size_t n_shades, size_t n_ri, size_t n_img, size_t n_tex,
+                    hipStream_t st, bool keep)
     {
         const size_t need[A_N] = {sizeof(RtNode) * n_slots, 8 * n_slots, 16 * n_slots, 4 * n_slots,
                                   sizeof(RtPrim) * list_used, sizeof(RtBvh) * bvh_used, 4 * list_used,
-                                  16 * list_used, sizeof(rt_shade) * n_shades, 4 * n_ent, 8 * n_ri};
+                                  16 * list_used, sizeof(rt_shade) * n_shades, 4 * n_ent, 8 * n_ri,
+                                  sizeof(RtImage) * n_img, n_tex};
         for (int k = 0; k < A_N; k++) {
             int r = a[k].reserve(need[k], keep ? a[k].cap : 0, st);
             if (r != RT_OK) return r;
@@ -359,6 +387,9 @@ struct RtSceneStore {
         d.shades = (const rt_shade *)a[A_SHADES].p;
         d.ent_sub = (const int32_t *)a[A_ENT_SUB].p;
         d.sub_ri = (const double *)a[A_SUB_RI].p;
+        d.images = (const RtImage *)a[A_IMAGES].p;
+        d.texels = (const uint8_t *)a[A_TEXELS].p;
+        d.n_images = (int32_t)m_images.size();
         d.n_nodes = (int32_t)slots.size();
         d.n_list = (int32_t)list_used;
         d.n_entities = s->n_entities;
@@ -432,14 +463,17 @@ struct RtSceneStore {
         bvh_used = bb;
         entity_mirrors(s);
         us.host_ms = ms_since(t0);
-        int r = reserve_all(N, s->n_entities, s->n_shades, s->n_substances, st, false);
+        pack_images(s, m_images, m_texels);
+        int r = reserve_all(N, s->n_entities, s->n_shades, s->n_substances, m_images.size(), m_texels.size(), st,
+                            false);
         if (r != RT_OK) return r;
         const void *src[A_N] = {m_node.data(), m_up.data(), m_ent.data(), m_dfs.data(), prim.data(),
-                                bvh.data(), m_list.data(), prefix.data(), s->shades, s->ent_substance, s->substance_ri};
+                                bvh.data(), m_list.data(), prefix.data(), s->shades, s->ent_substance, s->substance_ri,
+                                m_images.data(), m_texels.data()};
         const size_t bytes[A_N] = {sizeof(RtNode) * (size_t)N, 8 * (size_t)N, 16 * (size_t)N, 4 * (size_t)N,
                                    sizeof(RtPrim) * lb, sizeof(RtBvh) * bb, 4 * lb, 16 * lb,
                                    sizeof(rt_shade) * (size_t)s->n_shades, 4 * (size_t)s->n_entities,
-                                   8 * (size_t)s->n_substances};
+                                   8 * (size_t)s->n_substances, sizeof(RtImage) * m_images.size(), m_texels.size()};
         for (int k = 0; k < A_N; k++) {
             if (!bytes[k]) continue;
             HIP_TRY(hipMemcpyAsync(a[k].p, src[k], bytes[k], hipMemcpyHostToDevice, st));
@@ -536,7 +570,11 @@ struct RtSceneStore {
         // 4. capacities (keeping the resident contents), then the patches
         list_used = lu;
         bvh_used = bu;
-        int r = reserve_all(n_slots, NE, s->n_shades, s->n_substances, st, true);
+        std::vector<RtImage> n_images;
+        std::vector<uint8_t> n_texels;
+        pack_images(s, n_images, n_texels);
+        int r = reserve_all(n_slots, NE, s->n_shades, s->n_substances, n_images.size(),
+                            std::max(n_texels.size(), m_texels.size()), st, true);
         if (r != RT_OK) return r;
         m_list.resize(lu, -1);
         std::vector<RtPrim> recs, prim;
@@ -620,6 +658,14 @@ struct RtSceneStore {
             (s->n_substances && memcmp(m_ri.data(), s->substance_ri, 8 * (size_t)s->n_substances) != 0)) {
             m_ri.assign(s->substance_ri, s->substance_ri + s->n_substances);
             add(A_SUB_RI, 0, m_ri.data(), 8 * m_ri.size());
+        }
+        // images: resent whole when any changed (they are edited rarely)
+        if (n_images.size() != m_images.size() || n_texels != m_texels ||
+            (!n_images.empty() && memcmp(n_images.data(), m_images.data(), sizeof(RtImage) * n_images.size()) != 0)) {
+            m_images.swap(n_images);
+            m_texels.swap(n_texels);
+            add(A_IMAGES, 0, m_images.data(), sizeof(RtImage) * m_images.size());
+            add(A_TEXELS, 0, m_texels.data(), m_texels.size());
         }
         m_type.assign(s->ent_type, s->ent_type + NE);
         m_shade.assign(s->ent_shade, s->ent_shade + NE);

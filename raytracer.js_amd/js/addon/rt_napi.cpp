@@ -184,7 +184,7 @@ napi_value scene_call(napi_env env, napi_callback_info info, bool update)
     rt_ctx *ctx = unwrap(env, argv[0]);
     if (!ctx) return nullptr;
     napi_value s = argv[1];
-    Typed npos, nsize, npar, nch, nb, nc, list, et, eg, es, esub, sresp, slight, smirror, srough, srgb, ri;
+    Typed npos, nsize, npar, nch, nb, nc, list, et, eg, es, esub, sresp, slight, smirror, srough, srgb, ri, simg;
     if (!get_typed(env, s, "node_pos", napi_float64_array, npos, true) ||
         !get_typed(env, s, "node_size", napi_float64_array, nsize, true) ||
         !get_typed(env, s, "node_parent", napi_int32_array, npar, true) ||
@@ -203,10 +203,40 @@ napi_value scene_call(napi_env env, napi_callback_info info, bool update)
         !get_typed(env, s, "shade_rgb", napi_float64_array, srgb, true) ||
         !get_typed(env, s, "substance_ri", napi_float64_array, ri, true))
         return nullptr;
+    // ImageTextures: shade_image (Int32Array, optional) and images [{width, height, rgb: Uint8Array}]
+    bool has_simg = false;
+    napi_has_named_property(env, s, "shade_image", &has_simg);
+    if (has_simg && !get_typed(env, s, "shade_image", napi_int32_array, simg, true)) return nullptr;
+    std::vector<rt_image_desc> images;
+    bool has_images = false;
+    napi_has_named_property(env, s, "images", &has_images);
+    if (has_images) {
+        napi_value arr;
+        uint32_t ni = 0;
+        NAPI_TRY(napi_get_named_property(env, s, "images", &arr));
+        NAPI_TRY(napi_get_array_length(env, arr, &ni));
+        images.resize(ni);
+        for (uint32_t i = 0; i < ni; i++) {
+            napi_value im;
+            NAPI_TRY(napi_get_element(env, arr, i, &im));
+            double w = 0, h = 0;
+            Typed px;
+            if (!get_number(env, im, "width", w) || !get_number(env, im, "height", h) ||
+                !get_typed(env, im, "rgb", napi_uint8_array, px, true))
+                return nullptr;
+            if (px.length < (size_t)w * (size_t)h * 3) {
+                napi_throw_error(env, "RT_E_INVALID", "uploadScene: image rgb shorter than width*height*3");
+                return nullptr;
+            }
+            images[i].width = (int32_t)w;
+            images[i].height = (int32_t)h;
+            images[i].rgb = (const uint8_t *)px.data;
+        }
+    }
     const size_t n = nsize.length, ne = et.length, ns = sresp.length;
     if (npos.length != 3 * n || npar.length != n || nch.length != 8 * n || nb.length != n || nc.length != n ||
         eg.length != 9 * ne || es.length != ne || esub.length != ne || slight.length != ns || smirror.length != ns ||
-        srough.length != ns || srgb.length != 3 * ns) {
+        srough.length != ns || srgb.length != 3 * ns || (has_simg && simg.length != ns)) {
         napi_throw_error(env, "RT_E_INVALID", "uploadScene: inconsistent array lengths");
         return nullptr;
     }
@@ -218,6 +248,7 @@ napi_value scene_call(napi_env env, napi_callback_info info, bool update)
         sh.light = static_cast<int32_t *>(slight.data)[i];
         sh.mirror = static_cast<int32_t *>(smirror.data)[i];
         sh.roughness = static_cast<double *>(srough.data)[i];
+        sh.image = has_simg ? static_cast<int32_t *>(simg.data)[i] : 0;
         for (int k = 0; k < 3; k++) sh.rgb[k] = static_cast<double *>(srgb.data)[3 * i + k];
     }
     rt_scene_desc d;
@@ -240,6 +271,8 @@ napi_value scene_call(napi_env env, napi_callback_info info, bool update)
     d.ent_substance = (const int32_t *)esub.data;
     d.shades = shades.data();
     d.substance_ri = (const double *)ri.data;
+    d.n_images = (int32_t)images.size();
+    d.images = images.data();
     if (!update) {
         throw_rc(env, rt_upload_scene(ctx, &d));
         return nullptr;
@@ -298,9 +331,11 @@ napi_value TraceFrame(napi_env env, napi_callback_info info)
     cfg.default_substance = (int32_t)defsub;
     cfg.distance_attenuation_factor = att;
     cfg.col_weight = wgt;
-    double seed = 0, smode = RT_SCATTER_REJECT;
-    if (!get_number_opt(env, argv[2], "scatter_seed", seed) || !get_number_opt(env, argv[2], "scatter_mode", smode))
+    double seed = 0, smode = RT_SCATTER_REJECT, sky_image = 0;
+    if (!get_number_opt(env, argv[2], "scatter_seed", seed) || !get_number_opt(env, argv[2], "scatter_mode", smode) ||
+        !get_number_opt(env, argv[2], "sky_image", sky_image))
         return nullptr;
+    cfg.sky_image = (int32_t)sky_image;
     cfg.scatter_seed = seed > 0 ? (uint64_t)seed : 0;
     cfg.scatter_mode = (int32_t)smode;
     auto typed_arg = [&](size_t i, napi_typedarray_type want, Typed &t) -> bool {

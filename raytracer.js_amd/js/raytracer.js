@@ -49,8 +49,9 @@ function entity_kind(e) {
 }
 
 function solid_color(tex, what) {
-	// SolidTexture.get_size() is undefined (src/texture/texture_solid.ts:37-39); ImageTexture is
-	// outside the GPU path (SURVEY.md §2 row 7).
+	// SolidTexture.get_size() is undefined (src/texture/texture_solid.ts:37-39), as is an
+	// ImageTexture's (loaded ones are handled by loaded_image; an unloaded one shows its fallback
+	// colour through get_color).
 	if (!tex || typeof tex.get_color !== 'function' || (typeof tex.get_size === 'function' && tex.get_size() !== undefined)) {
 		const err = new Error('raytracer.js_amd: only SolidTexture is supported on the GPU path (' + what + ')');
 		err.code = 'RT_E_UNSUPPORTED';
@@ -58,6 +59,29 @@ function solid_color(tex, what) {
 	}
 	const c = tex.get_color(0, 0);
 	return [c.r, c.g, c.b];
+}
+
+/* ImageTexture after loading (src/texture/texture_image.ts:75-124): image_data holds the canvas
+ * bytes / 255.0, width x height texels of 3 values.  Before loading get_color returns the fallback
+ * colour, which the solid path handles. */
+function loaded_image(tex) {
+	return !!tex && tex.image_data != undefined && typeof tex.width === 'number' && typeof tex.height === 'number';
+}
+
+const image_bytes_cache = new WeakMap();
+function image_bytes(tex) {                     // the bytes back from image_data (exact: round(b / 255 * 255) = b)
+	const c = image_bytes_cache.get(tex);
+	if (c && c.data === tex.image_data) return c.bytes;
+	const n = tex.width * tex.height * 3;
+	if (tex.image_data.length < n) {
+		const err = new Error('raytracer.js_amd: ImageTexture image_data shorter than width*height*3');
+		err.code = 'RT_E_INVALID';
+		throw err;
+	}
+	const bytes = new Uint8Array(n);
+	for (let i = 0; i < n; i++) bytes[i] = Math.round(tex.image_data[i] * 255);
+	image_bytes_cache.set(tex, { data: tex.image_data, bytes });
+	return bytes;
 }
 
 function material_fields(m) {
@@ -82,7 +106,7 @@ function material_fields(m) {
  * stable — known objects keep their index, new ones are appended — which rt_update_scene needs to
  * send only what changed.
  */
-function serialize_scene(otree, default_substance, prev) {
+function serialize_scene(otree, default_substance, prev, sky_texture) {
 	if (otree.parent != undefined) {
 		const err = new Error('raytracer.js_amd: the Raytracer octree has a parent (it grew outward); not supported');
 		err.code = 'RT_E_UNSUPPORTED';
@@ -106,6 +130,13 @@ function serialize_scene(otree, default_substance, prev) {
 	const entities = prev ? prev.entities.slice() : [], list = [];
 	const ent_index = prev ? new Map(prev._maps.ent_index) : new Map();
 	const substances = prev ? prev.substances.slice() : [];
+	const images = prev ? prev._maps.images.slice() : [];
+	const image_index = prev ? new Map(prev._maps.image_index) : new Map();
+	const image_of = (tex) => {                  // rt_shade.image / sky_image: 1-based, 0 = solid
+		if (!loaded_image(tex)) return 0;
+		if (!image_index.has(tex)) { images.push(tex); image_index.set(tex, images.length); }
+		return image_index.get(tex);
+	};
 	const sub_index = prev ? new Map(prev._maps.sub_index) : new Map();
 	const sub_of = (s) => {
 		if (s == undefined) return -1;
@@ -179,13 +210,18 @@ function serialize_scene(otree, default_substance, prev) {
 	}
 	// every (material, texture) row is re-read: a host may have edited a material in place
 	for (const [m, per] of shade_index)
-		for (const [tex, i] of per) shades[i] = Object.assign(material_fields(m), { rgb: solid_color(tex, 'entity texture') });
+		for (const [tex, i] of per) {
+			const image = image_of(tex);
+			shades[i] = Object.assign(material_fields(m), { image, rgb: image ? [0, 0, 0] : solid_color(tex, 'entity texture') });
+		}
+	const sky_image = image_of(sky_texture);
 	const def_sub = sub_of(default_substance);
 	const ns = shades.length;
 	const shade_response = new Int32Array(ns), shade_light = new Int32Array(ns), shade_mirror = new Int32Array(ns);
-	const shade_roughness = new Float64Array(ns), shade_rgb = new Float64Array(3 * ns);
+	const shade_roughness = new Float64Array(ns), shade_rgb = new Float64Array(3 * ns), shade_image = new Int32Array(ns);
 	shades.forEach((s, i) => {
 		shade_response[i] = s.response; shade_light[i] = s.light; shade_mirror[i] = s.mirror;
+		shade_image[i] = s.image;
 		shade_roughness[i] = s.roughness;
 		shade_rgb[3 * i] = s.rgb[0]; shade_rgb[3 * i + 1] = s.rgb[1]; shade_rgb[3 * i + 2] = s.rgb[2];
 	});
@@ -193,9 +229,10 @@ function serialize_scene(otree, default_substance, prev) {
 	return {
 		node_pos, node_size, node_parent, node_child, node_ent_begin, node_ent_count,
 		list_entity: new Int32Array(list), ent_type, ent_geom, ent_shade, ent_substance,
-		shade_response, shade_light, shade_mirror, shade_roughness, shade_rgb, substance_ri,
-		entities, substances, default_substance_index: def_sub,
-		_maps: { ent_index, sub_index, shades, shade_index }
+		shade_response, shade_light, shade_mirror, shade_roughness, shade_rgb, shade_image, substance_ri,
+		images: images.map((t) => ({ width: t.width, height: t.height, rgb: image_bytes(t) })),
+		entities, substances, default_substance_index: def_sub, sky_image,
+		_maps: { ent_index, sub_index, shades, shade_index, images, image_index }
 	};
 }
 
@@ -252,11 +289,13 @@ class Raytracer {
 	_sync_scene() {
 		const a = load_addon();
 		if (!this._ctx) this._ctx = a.create(this.options.device | 0);
+		const sky = this.config.sky.texture;
+		if (this._scene && loaded_image(sky) && !this._scene._maps.image_index.has(sky)) this._dirty = true;
 		if (!this._scene) {
-			this._scene = serialize_scene(this.otree, this.config.default_substance);
+			this._scene = serialize_scene(this.otree, this.config.default_substance, undefined, sky);
 			a.uploadScene(this._ctx, this._scene);
 		} else if (this._dirty) {
-			this._scene = serialize_scene(this.otree, this.config.default_substance, this._scene);
+			this._scene = serialize_scene(this.otree, this.config.default_substance, this._scene, sky);
 			this.last_update = a.updateScene(this._ctx, this._scene);
 		}
 		this._dirty = false;
@@ -275,7 +314,8 @@ class Raytracer {
 		const cfg = {
 			refmax: this.config.refmax,
 			default_substance: scene.default_substance_index,
-			sky_rgb: solid_color(this.config.sky.texture, 'sky'),
+			sky_image: loaded_image(this.config.sky.texture) ? scene._maps.image_index.get(this.config.sky.texture) : 0,
+			sky_rgb: loaded_image(this.config.sky.texture) ? [0, 0, 0] : solid_color(this.config.sky.texture, 'sky'),
 			distance_attenuation_factor: this.config.distance_attenuation_factor,
 			col_weight: eb.col_weight
 		};

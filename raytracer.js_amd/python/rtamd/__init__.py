@@ -67,6 +67,8 @@ class SceneArrays:
         for k, dt in kinds.items():
             setattr(self, k, np.ascontiguousarray(arrays[k], dtype=dt).ravel())
         self.shades = np.ascontiguousarray(arrays["shades"], dtype=abi.SHADE_DTYPE)
+        # ImageTextures: [height, width, 3] uint8 each (image_data = bytes / 255.0)
+        self.images = [np.ascontiguousarray(im, dtype=np.uint8) for im in arrays.get("images", ())]
 
     @property
     def n_nodes(self):
@@ -79,6 +81,12 @@ class SceneArrays:
         d.n_entities = len(self.ent_type)
         d.n_shades = len(self.shades)
         d.n_substances = len(self.substance_ri)
+        d.n_images = len(self.images)
+        self._img = (abi.rt_image_desc * max(1, len(self.images)))()
+        for i, im in enumerate(self.images):
+            self._img[i].height, self._img[i].width = im.shape[0], im.shape[1]
+            self._img[i].rgb = im.ctypes.data_as(C.POINTER(C.c_uint8))
+        d.images = self._img
         for k in self.FIELDS:
             a = getattr(self, k)
             if k == "shades":
@@ -121,10 +129,12 @@ class Builder:
         self.h = b
         self.shades = np.zeros(0, abi.SHADE_DTYPE) if shades is None else np.ascontiguousarray(shades, abi.SHADE_DTYPE)
         self.substances = np.zeros(0) if substances is None else np.ascontiguousarray(substances, np.float64)
+        self.images = []
 
     @classmethod
     def from_spec(cls, spec):
         b = cls(spec.root_pos, spec.root_size, spec.shades, spec.substances)
+        b.images = list(spec.images)
         b.add(spec.entities)
         return b
 
@@ -154,7 +164,9 @@ class Builder:
         _check(self.L.rt_builder_desc(self.h, self.shades.ctypes.data_as(C.POINTER(abi.rt_shade)), len(self.shades),
                                       self.substances.ctypes.data_as(C.POINTER(C.c_double)), len(self.substances),
                                       C.byref(d)))
-        return _desc_to_arrays(d)
+        a = _desc_to_arrays(d)
+        a.images = list(self.images)
+        return a
 
 
 def build_scene(spec):
@@ -171,7 +183,9 @@ def build_scene(spec):
         d = abi.rt_scene_desc()
         _check(L.rt_builder_desc(b, shades.ctypes.data_as(C.POINTER(abi.rt_shade)), len(shades),
                                  ri.ctypes.data_as(C.POINTER(C.c_double)), len(ri), C.byref(d)))
-        return _desc_to_arrays(d)
+        a = _desc_to_arrays(d)
+        a.images = list(spec.images)
+        return a
     finally:
         L.rt_builder_destroy(b)
 

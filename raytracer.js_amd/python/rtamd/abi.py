@@ -30,22 +30,26 @@ _pi = C.POINTER(C.c_int32)
 
 
 class rt_shade(C.Structure):
-    _fields_ = [("response", _i), ("light", _i), ("mirror", _i), ("pad_", _i),
+    _fields_ = [("response", _i), ("light", _i), ("mirror", _i), ("image", _i),
                 ("roughness", _d), ("rgb", _d * 3)]
 
 
-SHADE_DTYPE = np.dtype([("response", "<i4"), ("light", "<i4"), ("mirror", "<i4"), ("pad_", "<i4"),
+SHADE_DTYPE = np.dtype([("response", "<i4"), ("light", "<i4"), ("mirror", "<i4"), ("image", "<i4"),
                         ("roughness", "<f8"), ("rgb", "<f8", (3,))])
 assert SHADE_DTYPE.itemsize == C.sizeof(rt_shade)
 
 
+class rt_image_desc(C.Structure):
+    _fields_ = [("width", _i), ("height", _i), ("rgb", C.POINTER(C.c_uint8))]
+
+
 class rt_scene_desc(C.Structure):
     _fields_ = [("n_nodes", _i), ("n_list", _i), ("n_entities", _i), ("n_shades", _i),
-                ("n_substances", _i), ("pad_", _i),
+                ("n_substances", _i), ("n_images", _i),
                 ("node_pos", _pd), ("node_size", _pd), ("node_parent", _pi), ("node_child", _pi),
                 ("node_ent_begin", _pi), ("node_ent_count", _pi), ("list_entity", _pi),
                 ("ent_type", _pi), ("ent_geom", _pd), ("ent_shade", _pi), ("ent_substance", _pi),
-                ("shades", C.POINTER(rt_shade)), ("substance_ri", _pd)]
+                ("shades", C.POINTER(rt_shade)), ("substance_ri", _pd), ("images", C.POINTER(rt_image_desc))]
 
 
 class rt_camera_desc(C.Structure):
@@ -56,7 +60,7 @@ class rt_camera_desc(C.Structure):
 class rt_config_desc(C.Structure):
     _fields_ = [("refmax", _i), ("default_substance", _i), ("sky_rgb", _d * 3),
                 ("distance_attenuation_factor", _d), ("col_weight", _d), ("scatter_seed", C.c_uint64),
-                ("scatter_mode", _i), ("pad_", _i)]
+                ("scatter_mode", _i), ("sky_image", _i)]
 
 
 RT_SCATTER_REJECT, RT_SCATTER_COUNTER = 0, 1

@@ -53,6 +53,7 @@ class SceneSpec:
     substances: np.ndarray = field(default_factory=lambda: SUBSTANCES.copy())
     root_pos: tuple = (0.0, 0.0, 0.0)
     root_size: float = 1.0
+    images: list = field(default_factory=list)   # ImageTextures, [H, W, 3] uint8 (rt_shade.image = k + 1)
 
 
 def _shade(response=abi.RT_RESP_REFLECTION, light=0, mirror=0, rgb=(1, 1, 1), roughness=0.0):
@@ -137,7 +138,30 @@ def roughen(spec, values=(0.05, 0.3, 0.8)):
     idx = np.nonzero(sh["mirror"])[0]
     for k, i in enumerate(idx):
         sh["roughness"][i] = values[k % len(values)]
-    return SceneSpec(spec.name + "_rough", spec.entities, sh, spec.substances, spec.root_pos, spec.root_size)
+    return SceneSpec(spec.name + "_rough", spec.entities, sh, spec.substances, spec.root_pos, spec.root_size,
+                     list(spec.images))
+
+
+def test_image(w, h, seed):
+    """A deterministic RGB image with sharp texel edges: a checkerboard over smooth gradients."""
+    u = Stream(seed).take(3)
+    y, x = np.mgrid[0:h, 0:w]
+    chk = ((x // max(1, w // 8) + y // max(1, h // 6)) & 1) * 96
+    img = np.stack([(x * 255 // max(1, w - 1) + chk) % 256, (y * 255 // max(1, h - 1) + 64 * u[0]) % 256,
+                    (chk + 128 * u[1] + 37 * x * y) % 256], axis=-1)
+    return img.astype(np.uint8)
+
+
+def texture(spec, images, every=2, sky=False):
+    """Copy of `spec` with ImageTextures: every `every`-th shade (lights excluded) samples one of
+    `images` instead of its SolidTexture colour (ImageTexture.get_color at entity.map_uv)."""
+    sh = spec.shades.copy()
+    imgs = list(spec.images) + list(images)
+    base = len(spec.images)
+    for i in range(len(sh)):
+        if i % every == 0 and not sh["light"][i]:
+            sh["image"][i] = base + 1 + (i // every) % len(images)
+    return SceneSpec(spec.name + "_tex", spec.entities, sh, spec.substances, spec.root_pos, spec.root_size, imgs)
 
 
 def random_triangles(st, n, half_extent, lo=0.02, hi=0.98, max_in_depth=6):
@@ -250,8 +274,10 @@ def make_camera(width, height, pos=(0.5, 0.5, 0.5), init_v=0.0, init_h=math.pi /
     return cam
 
 
-def make_config(refmax, sky=SKY_RGB, atten=1.0, default_substance=SUB_AIR, col_weight=1.0, scatter_seed=None):
-    """scatter_seed: None = RT_SCATTER_REJECT (rough mirrors unsupported), else RT_SCATTER_COUNTER."""
+def make_config(refmax, sky=SKY_RGB, atten=1.0, default_substance=SUB_AIR, col_weight=1.0, scatter_seed=None,
+                sky_image=0):
+    """scatter_seed: None = RT_SCATTER_REJECT (rough mirrors unsupported), else RT_SCATTER_COUNTER.
+    sky_image: 0 = SkySphere(SolidTexture(sky)), k = SkySphere of the scene's image k-1."""
     c = abi.rt_config_desc()
     c.refmax = int(refmax)
     c.default_substance = int(default_substance)
@@ -260,6 +286,7 @@ def make_config(refmax, sky=SKY_RGB, atten=1.0, default_substance=SUB_AIR, col_w
     c.col_weight = float(col_weight)
     c.scatter_mode = abi.RT_SCATTER_REJECT if scatter_seed is None else abi.RT_SCATTER_COUNTER
     c.scatter_seed = 0 if scatter_seed is None else int(scatter_seed) & (2 ** 64 - 1)
+    c.sky_image = int(sky_image)
     return c
 
 

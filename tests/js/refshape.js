@@ -21,6 +21,20 @@ class SolidTexture {
 	get_color(_u, _v) { return this.color; }
 	get_size() { return undefined; }
 }
+class ImageTexture {                       // a loaded ImageTexture: image_data = bytes / 255.0
+	constructor(width, height, bytes) {
+		this.width = width; this.height = height;
+		this.image_data = Array.from(bytes, (b) => b / 255.0);
+		this.fallback_color = { r: 1, g: 0, b: 1, a: 1 };
+	}
+	get_color(u, v) {
+		if (u < 0 - Number.EPSILON || u > 1 - Number.EPSILON || v < 0 - Number.EPSILON || v > 1 - Number.EPSILON)
+			throw Error('Texture coordinates out of bounds');
+		const i = (((v * this.height) << 0) * this.width + ((u * this.width) << 0)) * 3;
+		return { r: this.image_data[i], g: this.image_data[i + 1], b: this.image_data[i + 2], a: 1.0 };
+	}
+	get_size() { return undefined; }
+}
 class SolidMaterial {
 	constructor(response, light, mirror, roughness) { this.response = response; this.light_source = light; this.mirror = mirror; this.roughness_index = roughness; }
 	response_type(_) { return this.response; }
@@ -65,6 +79,7 @@ function inflate(sc) {
 		}
 	}
 	const subs = sc.substance_ri.map((ri) => new Substance(ri));
+	const images = (sc.images || []).map((im) => new ImageTexture(im.width, im.height, im.rgb));
 	const mats = new Map();
 	const ents = [];
 	for (let i = 0; i < sc.ent_type.length; i++) {
@@ -72,7 +87,7 @@ function inflate(sc) {
 		const key = [s.response, s.light, s.mirror, s.roughness].join(',');
 		if (!mats.has(key)) mats.set(key, new SolidMaterial(s.response, !!s.light, !!s.mirror, s.roughness));
 		const mat = mats.get(key);
-		const tex = new SolidTexture({ r: s.rgb[0], g: s.rgb[1], b: s.rgb[2], a: 1.0 });
+		const tex = s.image ? images[s.image - 1] : new SolidTexture({ r: s.rgb[0], g: s.rgb[1], b: s.rgb[2], a: 1.0 });
 		const sub = sc.ent_substance[i] >= 0 ? subs[sc.ent_substance[i]] : undefined;
 		const g = sc.ent_geom.slice(9 * i, 9 * i + 9);
 		let e;
@@ -86,7 +101,7 @@ function inflate(sc) {
 		const b = sc.node_ent_begin[k], c = sc.node_ent_count[k];
 		for (let j = b; j < b + c; j++) nodes[k].value.set.add(ents[sc.list_entity[j]]);
 	}
-	return { root: nodes[0], nodes, entities: ents, substances: subs };
+	return { root: nodes[0], nodes, entities: ents, substances: subs, images };
 }
 
 /** Camera-shaped object from an rt_camera_desc-like record. */
@@ -104,4 +119,4 @@ class ExposureBuffer {
 	clean_cache() { this.cleaned++; }
 }
 
-module.exports = { inflate, camera, ExposureBuffer, SolidTexture, Substance };
+module.exports = { ImageTexture, inflate, camera, ExposureBuffer, SolidTexture, Substance };

@@ -47,7 +47,8 @@ const cam = rs.camera(sc.cam);
 const eb = new rs.ExposureBuffer(sc.cam.width, sc.cam.height);
 const config = {
 	refmax: sc.cfg.refmax, default_substance: def_sub, distance_attenuation_factor: sc.cfg.atten,
-	sky: { texture: new rs.SolidTexture({ r: sc.cfg.sky[0], g: sc.cfg.sky[1], b: sc.cfg.sky[2], a: 1 }) }
+	sky: { texture: sc.cfg.sky_image ? world.images[sc.cfg.sky_image - 1]
+	                                 : new rs.SolidTexture({ r: sc.cfg.sky[0], g: sc.cfg.sky[1], b: sc.cfg.sky[2], a: 1 }) }
 };
 const si = process.argv.indexOf('--scatter');
 const seed = si > 0 ? Number(process.argv[si + 1]) : null;

@@ -30,21 +30,24 @@ def test_library_exports_every_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", rtamd.LIB_PATH], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r" T (rt_\w+)$", out, re.M))
     assert set(_declared()) <= exported
-    assert lib.rt_abi_version() == 2
+    assert lib.rt_abi_version() == 3
 
 
 def test_struct_layouts_match_header(tmp_path):
     prog = tmp_path / "sz.c"
-    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rt.h"\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n",'
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rt.h"\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n",'
                     'sizeof(rt_shade),sizeof(rt_scene_desc),sizeof(rt_camera_desc),sizeof(rt_config_desc),'
                     'sizeof(rt_stats),sizeof(rt_create_desc),sizeof(rt_entity_in),offsetof(rt_scene_desc,substance_ri),'
-                    'sizeof(rt_exposure_stats));return 0;}\n')
+                    'sizeof(rt_exposure_stats),sizeof(rt_image_desc),offsetof(rt_scene_desc,images),'
+                    'sizeof(rt_update_stats),offsetof(rt_config_desc,sky_image));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [C.sizeof(abi.rt_shade), C.sizeof(abi.rt_scene_desc), C.sizeof(abi.rt_camera_desc),
             C.sizeof(abi.rt_config_desc), C.sizeof(abi.rt_stats), C.sizeof(abi.rt_create_desc),
-            C.sizeof(abi.rt_entity_in), abi.rt_scene_desc.substance_ri.offset, C.sizeof(abi.rt_exposure_stats)]
+            C.sizeof(abi.rt_entity_in), abi.rt_scene_desc.substance_ri.offset, C.sizeof(abi.rt_exposure_stats),
+            C.sizeof(abi.rt_image_desc), abi.rt_scene_desc.images.offset, C.sizeof(abi.rt_update_stats),
+            abi.rt_config_desc.sky_image.offset]
     assert got == want
 
 

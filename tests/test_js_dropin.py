@@ -29,11 +29,13 @@ def _dump(tmp_path, spec, cam, cfg):
                                              "node_ent_count", "list_entity", "ent_type", "ent_geom", "ent_shade",
                                              "ent_substance", "substance_ri")}
     sc["shades"] = [dict(response=int(x["response"]), light=int(x["light"]), mirror=int(x["mirror"]),
-                         roughness=float(x["roughness"]), rgb=[float(v) for v in x["rgb"]]) for x in s.shades]
+                         roughness=float(x["roughness"]), image=int(x["image"]), rgb=[float(v) for v in x["rgb"]])
+                    for x in s.shades]
+    sc["images"] = [dict(width=int(im.shape[1]), height=int(im.shape[0]), rgb=im.reshape(-1).tolist()) for im in s.images]
     sc["cam"] = dict(width=cam.width, height=cam.height, pos=list(cam.pos), fr=list(cam.fr), lf=list(cam.lf),
                      up=list(cam.up), scan_h=list(cam.scan_h), scan_v=list(cam.scan_v))
     sc["cfg"] = dict(refmax=cfg.refmax, default_substance=cfg.default_substance, atten=cfg.distance_attenuation_factor,
-                     sky=list(cfg.sky_rgb))
+                     sky=list(cfg.sky_rgb), sky_image=int(cfg.sky_image))
     p = tmp_path / "scene.json"
     p.write_text(json.dumps(sc))
     return str(p)
@@ -57,21 +59,30 @@ def test_serialize_matches_native_builder(tmp_path, name):
 def test_addon_loads_and_fails_loudly_without_gpu():
     """The addon loads; with no GPU create() throws RT_E_NODEVICE (never a silent CPU path)."""
     js = ("const rt=require(%r);const a=rt.load_addon();"
-          "if(a.abiVersion()!==2)throw Error('abi');"
+          "if(a.abiVersion()!==3)throw Error('abi');"
           "try{a.create(0);console.log('GPU')}catch(e){console.log(e.code)}") % os.path.join(ROOT, "raytracer.js_amd", "js", "raytracer.js")
     out = _node(["-e", js]).strip()
     assert out in ("GPU", "RT_E_NODEVICE")
 
 
+def _textured_open(seed):
+    s = scenes.small_random(seed, n_sph=80)
+    s = scenes.SceneSpec(s.name, s.entities[:-1], s.shades, s.substances, s.root_pos, s.root_size)   # no room box
+    return scenes.texture(s, [scenes.test_image(64, 32, 1), scenes.test_image(33, 17, 2)], every=2)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,wh,refmax", [("config1", (256, 256), 2), ("small4", (200, 150), 3),
-                                            ("small4_rough", (200, 150), 4)])
+                                            ("small4_rough", (200, 150), 4), ("small5_tex", (160, 120), 3)])
 def test_dropin_frame_equals_oracle(tmp_path, name, wh, refmax):
-    """small4_rough: rough mirrors through options.scatter = 'counter' (RT_SCATTER_COUNTER)."""
+    """small4_rough: rough mirrors through options.scatter = 'counter' (RT_SCATTER_COUNTER);
+    small5_tex: loaded ImageTextures on entities and the SkySphere."""
     spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4),
-            "small4_rough": lambda: scenes.roughen(scenes.small_random(4, p_mirror=0.5))}[name]()
+            "small4_rough": lambda: scenes.roughen(scenes.small_random(4, p_mirror=0.5)),
+            "small5_tex": lambda: _textured_open(5)}[name]()
     seed = 123456789012345 if name.endswith("rough") else None
-    cam, cfg = scenes.make_camera(*wh), scenes.make_config(refmax, scatter_seed=seed)
+    cam = scenes.make_camera(*wh)
+    cfg = scenes.make_config(refmax, scatter_seed=seed, sky_image=2 if name.endswith("tex") else 0)
     path = _dump(tmp_path, spec, cam, cfg)
     _node([RUNNER, path, str(tmp_path / "out")] + (["--scatter", str(seed)] if seed else []))
     P = wh[0] * wh[1]
