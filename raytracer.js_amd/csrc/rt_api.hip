@@ -72,6 +72,9 @@ struct rt_ctx {
     bool split = true;               // walk pass + test pass (RT_SPLIT=0: fused k_trace)
     int cand_cap = 64;               // candidate nodes per pixel in the split path (RT_CAND_CAP)
     int split_levels = RT_MAX_LEVELS + 1;   // split-path bounce levels (RT_SPLIT_LEVELS)
+    int claim_chunk = 1;             // items per queue claim in the short passes (RT_CLAIM_CHUNK)
+    int xcd_mask = 0;                // passes claiming per-XCD bands (RT_XCD: 1 walk, 2 first, 4 shade)
+    int shade_occ = 3;               // k_shade occupancy variant (RT_SHADE_OCC)
     int cont_group = 8;              // continuation rays per wave (RT_CONT_GROUP): their passes are
                                      // latency-bound, fewer lanes per wave shorten the slowest wave
     int occ = 0;
@@ -112,6 +115,9 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_SPLIT")) c->split = atoi(e) != 0;
     if (c->flags & RT_CREATE_NO_SPLIT) c->split = false;
     if (const char *e = getenv("RT_CAND_CAP")) c->cand_cap = atoi(e) < 1 ? 1 : atoi(e);
+    if (const char *e = getenv("RT_XCD")) c->xcd_mask = atoi(e) & 7;
+    if (const char *e = getenv("RT_SHADE_OCC")) c->shade_occ = atoi(e);
+    if (const char *e = getenv("RT_CLAIM_CHUNK")) c->claim_chunk = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_SPLIT_LEVELS")) c->split_levels = atoi(e) < 1 ? 1 : atoi(e);
     if (const char *e = getenv("RT_CONT_GROUP")) c->cont_group = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
@@ -230,6 +236,9 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.diag = c->diag;
     L.cont_group = c->cont_group;
     L.split_levels = c->split_levels;
+    L.claim_chunk = c->claim_chunk;
+    L.xcd_mask = c->xcd_mask;
+    L.shade_occ = c->shade_occ;
     if (c->split && P > 0) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).

@@ -129,9 +129,12 @@ struct RtLaunch {
     int32_t level, last_level;                  // set per launch by rt_launch_frame
     int32_t cont_group;                         // continuation rays per wave (levels >= 1)
     int32_t split_levels;                       // bounce levels on the split path; deeper ones run in k_cont
+    int32_t claim_chunk;                        // work items per queue claim in k_first / k_shade
+    int32_t xcd_mask;                           // passes with per-XCD work bands: 1 walk, 2 first, 4 shade
+    int32_t shade_occ;                          // k_shade waves per SIMD the registers must admit (3, 4, 5)
 };
 
-enum { RT_MAX_LEVELS = 32, RT_CTR_INTS = 4 + 4 * (RT_MAX_LEVELS + 1) };
+enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };
 
 int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end);
 // rt_exposure.hip: statistics into d_out3 = {mean, variance, absdev} (d_partials: 2 * n_blocks doubles)

@@ -128,7 +128,7 @@ RT_HD double js_atan2(double y, double x)
     const uint32_t lx = lo_word(x), ly = lo_word(y);
     if ((ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000u || (iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000u)
         return x + y;                                // NaN
-    if (((uint32_t)hx - 0x3ff00000u | lx) == 0) return js_atan(y);   // x == 1.0
+    if ((((uint32_t)hx - 0x3ff00000u) | lx) == 0) return js_atan(y);   // x == 1.0
     int m = (int)(((uint32_t)hy >> 31) & 1u) | (int)(((uint32_t)hx >> 30) & 2u);   // 2*sign(x) + sign(y)
     if ((iy | ly) == 0) {                            // y = +-0
         switch (m) {

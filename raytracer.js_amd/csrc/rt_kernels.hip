@@ -694,11 +694,22 @@ struct RayQueues {
     bool last;                 // no next level: continuations go to ovf
 };
 
+// One queue slot per active lane with a single atomic per wave: the lanes that reach a push are
+// exactly the active ones, so the first of them reserves the slots for all (ballot + rank).
+__device__ __forceinline__ int wave_reserve(int32_t *qn)
+{
+    const unsigned long long active = __ballot(1);
+    const int rank = __popcll(active & ((1ull << __lane_id()) - 1));
+    int base = 0;
+    if (rank == 0) base = atomicAdd(qn, __popcll(active));
+    return __builtin_amdgcn_readfirstlane(base) + rank;
+}
+
 __device__ __forceinline__ void queue_push(RtCont *q, int32_t *qn, const double o[3], const double d[3], double col0,
                                            double col1, double col2, double path, int refcount, int cur_sub,
                                            const RayResult &R, int pix, int fresh, uint32_t draws)
 {
-    const int k = atomicAdd(qn, 1);
+    const int k = wave_reserve(qn);
     RtCont &e = q[k];
     for (int i = 0; i < 3; i++) { e.o[i] = o[i]; e.d[i] = d[i]; }
     e.col[0] = col0; e.col[1] = col1; e.col[2] = col2;
@@ -964,15 +975,52 @@ __device__ __forceinline__ void write_pixel(const RtLaunch &L, size_t pix, const
 
 // ---- work distribution ------------------------------------------------------------------------------------
 // Device counters (L.ctr): [0] overflow queue count, [1] its read head; per level lv (0 = primary
-// rays, >= 1 = continuation levels) a block at 4 + 4*lv: {count of the queue written at this
-// level, work head of k_walk, of k_first, of k_shade}.  Level lv reads queue (lv-1)&1 and writes
-// queue lv&1.
-__device__ __forceinline__ int32_t *lvl_ctr(const RtLaunch &L, int lv) { return L.ctr + 4 + 4 * lv; }
+// rays, >= 1 = continuation levels) a block of RT_CTR_LEVEL at 4 + RT_CTR_LEVEL*lv: [0] the count
+// of the queue written at this level, [8p .. 8p+7] the per-XCD work heads of pass p (1 k_walk,
+// 2 k_first, 3 k_shade).  Level lv reads queue (lv-1)&1 and writes queue lv&1.
+__device__ __forceinline__ int32_t *lvl_ctr(const RtLaunch &L, int lv) { return L.ctr + 4 + RT_CTR_LEVEL * lv; }
 
-__device__ __forceinline__ int claim(int32_t *head, int lane)
+// The 8 per-XCD claim heads of pass p (1 walk, 2 first, 3 shade) at level lv.
+__device__ __forceinline__ int32_t *pass_heads(const RtLaunch &L, int lv, int p) { return lvl_ctr(L, lv) + 8 * p; }
+
+// XCD-aware work claim.  Each XCD (its own 4 MB L2) owns one contiguous eighth of the items —
+// a horizontal band of the frame at level 0 — so the rays sharing an L2 share their scene working
+// set; an XCD whose band is done steals from the others.  The XCD is read from HW_REG_XCC_ID (gfx950
+// dispatches workgroups round-robin, but the register is authoritative).  Returns the first item
+// of a run of up to n in one band, *end = one past its last; items when everything is claimed.
+__device__ __forceinline__ int claim_xcd(int32_t *heads, int items, int lane, int n, int &end, bool xcd)
+{
+    int t = items, e = items;
+    if (!xcd) {                                   // one queue over all items
+        if (lane == 0) {
+            t = atomicAdd(&heads[0], n);
+            e = t + n < items ? t + n : items;
+        }
+        end = __builtin_amdgcn_readfirstlane(__shfl(e, 0, 64));
+        return __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+    }
+    if (lane == 0) {
+        const int x = (int)(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7);   // HW_REG_XCC_ID
+        for (int k = 0; k < 8; k++) {
+            const int y = (x + k) & 7;
+            const int lo = (int)((long long)items * y >> 3), size = (int)((long long)items * (y + 1) >> 3) - lo;
+            if (__hip_atomic_load(&heads[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= size) continue;
+            const int u = atomicAdd(&heads[y], n);
+            if (u < size) {
+                t = lo + u;
+                e = lo + (u + n < size ? u + n : size);
+                break;
+            }
+        }
+    }
+    end = __builtin_amdgcn_readfirstlane(__shfl(e, 0, 64));
+    return __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+}
+
+__device__ __forceinline__ int claim(int32_t *head, int lane, int n = 1)
 {
     int t = 0;
-    if (lane == 0) t = atomicAdd(head, 1);
+    if (lane == 0) t = atomicAdd(head, n);
     return __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
 }
 
@@ -1036,7 +1084,8 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
     const ListHit none = {-1, -1, 0};
     const RayQueues Q = {nullptr, nullptr, nullptr, nullptr, false};
     for (;;) {
-        const int t = claim(lvl_ctr(L, 0) + 1, lane);
+        int t_end;
+        const int t = claim_xcd(pass_heads(L, 0, 1), n_tiles, lane, 1, t_end, L.xcd_mask & 1);
         if (t >= n_tiles) break;
         const long long t_tile = (STATS && (L.diag & 8)) ? (long long)clock64() : 0;
         RaySrc src;
@@ -1090,7 +1139,8 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (;;) {
-        const int t = claim(lvl_ctr(L, L.level) + 1, lane);
+        int t_end;
+        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
         if (t >= items) break;
         RaySrc src;
         ray_src(L, t, lane, src);
@@ -1134,9 +1184,12 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const bool fault = L.setup->fault != 0;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const int ch = L.claim_chunk;
     for (;;) {
-        const int t = claim(lvl_ctr(L, L.level) + 2, lane);
-        if (t >= items) break;
+        int t_end;
+        const int t0 = claim_xcd(pass_heads(L, L.level, 2), items, lane, ch, t_end, L.xcd_mask & 2);
+        if (t0 >= items) break;
+        for (int t = t0; t < t_end; t++) {
         RaySrc src;
         ray_src(L, t, lane, src);
         if (!src.valid) continue;
@@ -1156,6 +1209,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
             }
         }
         reinterpret_cast<int2 *>(L.first)[src.id] = res;
+        }
     }
 }
 
@@ -1169,9 +1223,12 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
     const RtFrameSetup F = *L.setup;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const RayQueues Q = {L.queue[L.level & 1], lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
+    const int ch = L.claim_chunk;
     for (;;) {
-        const int t = claim(lvl_ctr(L, L.level) + 3, lane);
-        if (t >= items) break;
+        int t_end;
+        const int t0 = claim_xcd(pass_heads(L, L.level, 3), items, lane, ch, t_end, L.xcd_mask & 4);
+        if (t0 >= items) break;
+        for (int t = t0; t < t_end; t++) {
         RaySrc src;
         ray_src(L, t, lane, src);
         if (!src.valid) continue;
@@ -1185,7 +1242,7 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
         if (cn < 0) {
             // the candidate list overflowed: the fused kernel traces this ray (from its segment start)
             if (src.rec) {
-                const int k = atomicAdd(L.ctr, 1);
+                const int k = wave_reserve(L.ctr);
                 L.ovf[k] = *src.rec;
             } else {
                 R.hit_ent = -1; R.hit_node = -1; R.segments = 1;
@@ -1199,6 +1256,7 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
                                   src.pix, L);
         if (R.status == ST_DEFER) continue;
         write_pixel(L, (size_t)src.pix, R);
+        }
     }
 }
 
@@ -1312,7 +1370,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             HIP_TRY(hipGetLastError());
             launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv);
             HIP_TRY(hipGetLastError());
-            launch_persistent(k_shade<3>, st, Lv);
+            launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv);
             HIP_TRY(hipGetLastError());
         }
         launch_persistent(k_cont<3>, st, L);
