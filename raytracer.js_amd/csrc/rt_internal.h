@@ -10,21 +10,33 @@ int rt_set_error(int code, const char *fmt, ...);
 
 // ---- device scene layout (HBM) ---------------------------------------------------------------
 // Node records are split by access pattern (SoA of small records):
-//   node      RtNode   {pos.x, pos.y, pos.z, size, child[8]}   read by update_next_pos / step_in /
-//                                                            every walker slot visit
+//   node      RtNode   128 B {pos.xyz, size, child[8], cull root box, entity count}: read by
+//                      update_next_pos / step_in / every slot visit / the walk pass's candidate test
 //   node_up   int2     {parent, index_within_parent}     read by step_back
 //   node_ent  int2     {list begin, count}               read when a node is returned
 // Primitives are re-packed in list order (each entity appears in exactly one EntitySet), so a
 // node's entity scan streams one contiguous run of 80-byte records.
 enum : int { RT_OCT_UNDEF = -1, RT_OCT_BAD = 1000 };
 
-// A node's cube and its children in one 64-byte record: a step-in reads the child's cube, and the
-// next slot visit its child ids, from the same cache line.
-struct alignas(64) RtNode {
+struct alignas(16) RtBvh {
+    float lo[3], hi[3];
+    int32_t skip;      // next node when this subtree is done or culled; -1 = end of this node's tree
+    int32_t info;      // leaf: first prim slot << 4 | count (1..15); inner: -1
+};
+static_assert(sizeof(RtBvh) == 32, "RtBvh must stay 32 bytes");
+
+// Everything the walk pass reads about a node in one 128-byte cache line: its cube and children
+// (a step-in reads the child's cube, the next slot visit its child ids), its entity count and the
+// root box of its cull hierarchy (the candidate test of a returned node), so a returned node costs
+// one line, which the step-in that follows finds in cache.
+struct alignas(128) RtNode {
     double x, y, z, s;      // OctreeDim.pos, size
     int32_t child[8];       // child slot per octant, -1 = empty
+    RtBvh box;              // copy of the cull-hierarchy root record (lo/hi); unused when n_ent == 0
+    int32_t n_ent;          // EntitySet size
+    int32_t pad_[7];
 };
-static_assert(sizeof(RtNode) == 64, "RtNode must stay 64 bytes");
+static_assert(sizeof(RtNode) == 128, "RtNode must stay 128 bytes");
 
 // A loaded ImageTexture (rt_image_desc): width x height RGB bytes at texels + offset.
 struct RtImage {
@@ -45,13 +57,6 @@ static_assert(sizeof(RtPrim) == 80, "RtPrim must stay 80 bytes");
 // depth-first order with skip links (stackless).  Bounds are the entities' AABBs widened by a
 // margin and rounded outward to f32, so a ray that the exact binary64 test can report as hitting
 // an entity always passes its box.  Inner node: first child = this + 1.
-struct alignas(16) RtBvh {
-    float lo[3], hi[3];
-    int32_t skip;      // next node when this subtree is done or culled; -1 = end of this node's tree
-    int32_t info;      // leaf: first prim slot << 4 | count (1..15); inner: -1
-};
-static_assert(sizeof(RtBvh) == 32, "RtBvh must stay 32 bytes");
-
 // Nodes live in stable slots (rt_scene.hip): slot 0 is the root; after incremental updates slot
 // order is no longer DFS order, node_dfs maps back.
 struct RtDevScene {

@@ -525,11 +525,23 @@ __device__ __forceinline__ int prim_hit(const RtPrim &pr, const double o[3], con
 // Returns the prim slot or -1; *rank_out receives its rank.
 template <bool STATS>
 __device__ int node_first_hit(const RtDevScene &S, const int4 ne, const double o[3], const double d[3],
-                              const RayBox &rb, bool cull, Counters &c, long long &box_ctr, Hit &h, int &rank_out)
+                              const RayBox &rb, bool cull, Counters &c, long long &box_ctr, Hit &h, int &rank_out,
+                              bool root_hit = false)
 {
     int best_rank = 0x7fffffff, best_slot = -1;
     if (cull && rb.ok) {
+        // root_hit: the walk pass already found the root box crossed (the same RayBox test), so
+        // start at its first child (DFS layout: root + 1), or at the single prim of a leaf root
         int i = ne.z;
+        if (root_hit) {
+            if (ne.y == 1) {
+                c.exact++;
+                if (prim_hit(S.prim[ne.x], o, d, h)) { best_rank = S.prim[ne.x].rank; best_slot = ne.x; }
+                i = -1;
+            } else {
+                i = ne.z + 1;
+            }
+        }
         while (i >= 0) {
             const RtBvh b = S.bvh[i];
             box_ctr++;
@@ -1159,9 +1171,9 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
                 const int r = walker_next<false>(S, w, node, pt, po, c);
                 if (r < 0) { end = r == -2 ? 2 : 1; break; }
                 if (r == 0) break;
-                const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
-                if (ent.y == 0) continue;
-                if (L.cull && rb.ok && !ray_box(S.bvh[ent.z], rb)) continue;
+                const RtNode &nd = S.node[node];               // one cache line: count + root box
+                if (nd.n_ent == 0) continue;
+                if (L.cull && rb.ok && !ray_box(nd.box, rb)) continue;
                 if (n < L.cand_cap) L.cand[(size_t)n * stride + src.id] = node;
                 n++;
             }
@@ -1204,7 +1216,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
                 Hit h;
                 int rank;
                 long long box = 0;
-                const int hk = node_first_hit<false>(S, ent, src.o, src.d, rb, L.cull != 0, c, box, h, rank);
+                const int hk = node_first_hit<false>(S, ent, src.o, src.d, rb, L.cull != 0, c, box, h, rank, true);
                 if (hk >= 0) { res = make_int2(node, hk); break; }
             }
         }
@@ -1271,11 +1283,12 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const ListHit none = {-1, -1, 0};
     const RayQueues Q = {nullptr, nullptr, nullptr, nullptr, false};
+    const int g = L.cont_group;                   // rays per wave: these rays are few and long
     for (;;) {
-        const int base = claim(L.ctr + 1, lane) * 64;
+        const int base = claim(L.ctr + 1, lane) * g;
         if (base >= n) break;
         const int q = base + lane;
-        if (q >= n) continue;
+        if (lane >= g || q >= n) continue;
         const RtCont *e = L.ovf + q;
         RayResult R;
         trace_ray<false, TR_FUSED>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, e->d, R, c, -1, none, e, Q,

@@ -434,6 +434,7 @@ struct RtSceneStore {
         size_t lb = 0, bb = 0;
         for (int n = 0; n < N; n++) {
             RtNode &nd = m_node[n];
+            nd = RtNode{};
             nd.x = s->node_pos[3 * n]; nd.y = s->node_pos[3 * n + 1]; nd.z = s->node_pos[3 * n + 2];
             nd.s = s->node_size[n];
             for (int k = 0; k < 8; k++) nd.child[k] = s->node_child[8 * (size_t)n + k];
@@ -452,6 +453,8 @@ struct RtSceneStore {
                                                      &prim[lb], &bvh[bb], &prefix[4 * lb])
                                 : -1;
             slots[n] = {(int32_t)lb, c, c, (int32_t)bb, c ? 2 * c - 1 : 0, broot};
+            nd.n_ent = c;
+            if (c) nd.box = bvh[bb];
             m_ent[4 * n] = (int32_t)lb;
             m_ent[4 * n + 1] = c;
             m_ent[4 * n + 2] = broot;
@@ -577,6 +580,7 @@ struct RtSceneStore {
                             std::max(n_texels.size(), m_texels.size()), st, true);
         if (r != RT_OK) return r;
         m_list.resize(lu, -1);
+        m_node.resize(n_slots);                       // new slots start zeroed
         std::vector<RtPrim> recs, prim;
         std::vector<RtBvh> bvh;
         std::vector<int32_t> prefix;
@@ -604,11 +608,12 @@ struct RtSceneStore {
             m_ent[4 * dd.sl + 1] = c;
             m_ent[4 * dd.sl + 2] = S.broot;
             m_ent[4 * dd.sl + 3] = 0;
+            m_node[dd.sl].n_ent = c;
+            m_node[dd.sl].box = c ? bvh[0] : RtBvh{};
         }
         // node records: new slots, and the existing parents that gained a child (an existing node's
         // cube, parent and octant never change); node_dfs wherever the DFS numbering shifted
         std::vector<int32_t> touched;                 // slots whose ps / child / up records are rewritten
-        m_node.resize(n_slots);
         m_up.resize(2 * n_slots);
         std::vector<int32_t> n_dfs(m_dfs);
         n_dfs.resize(n_slots);
@@ -638,7 +643,6 @@ struct RtSceneStore {
                 m_node[sl].child[k] = ch < 0 ? -1 : slot_of_dfs[ch];
             }
         }
-        add_slots(A_NODE, touched, m_node.data(), sizeof(RtNode));
         add_slots(A_NODE_UP, touched, m_up.data(), 2 * sizeof(int32_t));
         diff_runs(A_NODE_DFS, n_dfs, m_dfs, 1);
         std::vector<int32_t> ent_slots;
@@ -646,6 +650,12 @@ struct RtSceneStore {
         for (const Dirty &dd : dirty) ent_slots.push_back(dd.sl);
         std::sort(ent_slots.begin(), ent_slots.end());
         add_slots(A_NODE_ENT, ent_slots, m_ent.data(), 4 * sizeof(int32_t));
+        // node records: new / re-parented slots and the dirty ones (entity count, root box)
+        std::vector<int32_t> rec_slots(touched);
+        rec_slots.insert(rec_slots.end(), ent_slots.begin(), ent_slots.end());
+        std::sort(rec_slots.begin(), rec_slots.end());
+        rec_slots.erase(std::unique(rec_slots.begin(), rec_slots.end()), rec_slots.end());
+        add_slots(A_NODE, rec_slots, m_node.data(), sizeof(RtNode));
         // entity substances and the shade / substance tables
         std::vector<int32_t> n_sub(s->ent_substance, s->ent_substance + NE);
         diff_runs(A_ENT_SUB, n_sub, m_sub, 1);
