@@ -34,7 +34,9 @@ struct alignas(128) RtNode {
     int32_t child[8];       // child slot per octant, -1 = empty
     RtBvh box;              // copy of the cull-hierarchy root record (lo/hi); unused when n_ent == 0
     int32_t n_ent;          // EntitySet size
-    int32_t pad_[7];
+    int32_t up_tree;        // parent slot (-1: root) — step_back
+    int32_t up_oct;         // index_within_parent (RT_OCT_UNDEF for the root, RT_OCT_BAD if not 0..7)
+    int32_t pad_[5];
 };
 static_assert(sizeof(RtNode) == 128, "RtNode must stay 128 bytes");
 

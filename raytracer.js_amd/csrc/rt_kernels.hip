@@ -347,7 +347,8 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
         } else {
             if (w.depth > 0) { w.depth--; w.flags |= F_RET; }
             else w.flags &= ~F_RET;
-            const int2 up = reinterpret_cast<const int2 *>(S.node_up)[w.cur_tree];
+            const RtNode &nd = S.node[w.cur_tree];             // the line update_next_pos just read
+            const int2 up = make_int2(nd.up_tree, nd.up_oct);
             if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
             else w.cur_oct = RT_OCT_UNDEF;
         }

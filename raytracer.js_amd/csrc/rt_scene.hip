@@ -440,6 +440,8 @@ struct RtSceneStore {
             for (int k = 0; k < 8; k++) nd.child[k] = s->node_child[8 * (size_t)n + k];
             m_up[2 * n] = n == 0 ? -1 : s->node_parent[n];
             m_up[2 * n + 1] = oct[n];
+            nd.up_tree = m_up[2 * n];
+            nd.up_oct = oct[n];
             m_dfs[n] = n;
             m_order[n] = n;
             slot_of.emplace(node_key(s, n), n);
@@ -629,6 +631,8 @@ struct RtSceneStore {
             nd.s = s->node_size[n];
             m_up[2 * (size_t)sl] = n == 0 ? -1 : slot_of_dfs[s->node_parent[n]];
             m_up[2 * (size_t)sl + 1] = oct[n];
+            nd.up_tree = m_up[2 * (size_t)sl];
+            nd.up_oct = oct[n];
             if (n > 0 && slot_of_dfs[s->node_parent[n]] < (int)n_old) touched.push_back(slot_of_dfs[s->node_parent[n]]);
             slot_of.emplace(node_key(s, n), sl);
         }
