@@ -1213,7 +1213,8 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
             const int n = cn >> 2;
             for (int k = 0; k < n; k++) {
                 const int node = L.cand[(size_t)k * stride + src.id];
-                const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
+                const RtNode &nd = S.node[node];               // the line k_walk read for this candidate
+                const int4 ent = make_int4(nd.ent_begin, nd.n_ent, nd.bvh_root, 0);
                 Hit h;
                 int rank;
                 long long box = 0;

@@ -456,6 +456,8 @@ struct RtSceneStore {
                                 : -1;
             slots[n] = {(int32_t)lb, c, c, (int32_t)bb, c ? 2 * c - 1 : 0, broot};
             nd.n_ent = c;
+            nd.ent_begin = (int32_t)lb;
+            nd.bvh_root = broot;
             if (c) nd.box = bvh[bb];
             m_ent[4 * n] = (int32_t)lb;
             m_ent[4 * n + 1] = c;
@@ -611,6 +613,8 @@ struct RtSceneStore {
             m_ent[4 * dd.sl + 2] = S.broot;
             m_ent[4 * dd.sl + 3] = 0;
             m_node[dd.sl].n_ent = c;
+            m_node[dd.sl].ent_begin = S.lbeg;
+            m_node[dd.sl].bvh_root = S.broot;
             m_node[dd.sl].box = c ? bvh[0] : RtBvh{};
         }
         // node records: new slots, and the existing parents that gained a child (an existing node's
