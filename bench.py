@@ -4,6 +4,13 @@ A step is one frame: ray generation + trace + (N>1) RCCL gather of the row strip
 de-interleave into the 1920x1080 frame.  The frame is split across ranks (strong scaling: the
 frame size is fixed).  Inputs (scene, camera) are resident on the GPU before the timed region.
 
+Frames in flight (--inflight P, default 4): each rank keeps P contexts, each on its own HIP
+stream with its own frame buffers, and issues frame f on context f % P.  A frame's bounce level 1
+is a latency-bound tail (few, long continuation rays) that the next frames' primary
+passes fill.  Every one of the K timed frames is rendered and gathered completely inside the timed
+region; `value` is their throughput.  A serial pass (one frame in flight) reports the per-frame
+latency beside it (`serial`) and is what the roofline's kernel duration is measured on.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config config3]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
@@ -175,6 +182,7 @@ def main():
     ap.add_argument("--stripe", type=int, default=8, help="rows per stripe of the row-interleaved split")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
+    ap.add_argument("--inflight", type=int, default=4, help="frames in flight per rank (contexts / streams)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
@@ -193,21 +201,51 @@ def main():
     t0 = time.perf_counter()
     scene = rtamd.build_scene(spec)
     build_s = time.perf_counter() - t0
-    ctx = rtamd.Context(local)
-    ctx.upload(scene)
+    P = max(1, min(args.inflight, args.steps))
+    ctxs = []
+    for _ in range(P):
+        c = rtamd.Context(local)
+        c.upload(scene)
+        ctxs.append(c)
+    ctx = ctxs[0]
     cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
-    # one explicit stream for librt launches, torch copies and the collectives (the legacy NULL
-    # stream would not order against librt's non-blocking stream)
-    stream = torch.cuda.Stream(device=dev)
+    # explicit streams for librt launches, torch copies and the collectives (the legacy NULL
+    # stream would not order against librt's non-blocking stream); frame f uses slot f % P
+    streams = [torch.cuda.Stream(device=dev) for _ in range(P)]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
-
-    sg = StripeGather(H, W, rank, world, args.stripe, dev)
+    sgs = [StripeGather(H, W, rank, world, args.stripe, dev) for _ in range(P)]
+    sg = sgs[0]
     local_buf = sg.local
 
-    def step():
-        ctx.trace_rows_device(cam, cfg, rank, world, args.stripe, local_buf.data_ptr(), sp)
-        sg.gather()
+    def step(f, inflight):
+        i = f % inflight
+        with torch.cuda.stream(streams[i]):
+            ctxs[i].trace_rows_device(cam, cfg, rank, world, args.stripe, sgs[i].local.data_ptr(),
+                                      streams[i].cuda_stream)
+            sgs[i].gather()        # the collective waits for this stream; this stream for it
+
+    def timed(inflight, steps, warmup):
+        for f in range(warmup):
+            step(f, inflight)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for f in range(steps):
+            step(f, inflight)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
     # work counters of one frame (untimed STATS launch): segments and algorithmic bytes
     _, st = ctx.trace_rows_device(cam, cfg, rank, world, args.stripe, local_buf.data_ptr(), sp, stats=True)
@@ -220,29 +258,19 @@ def main():
     local_bytes = algorithmic_bytes(counters, BYTES_KERNEL)
     local_bytes_ref = algorithmic_bytes(counters, BYTES_REF)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(P, args.steps, max(args.warmup, P))
+    # every in-flight slot rendered the same camera: their gathered frames must agree bit for bit
+    same = all(torch.equal(sgs[i].frame.view(torch.int32), sgs[0].frame.view(torch.int32)) for i in range(1, P)) \
+        if rank == 0 else None
+    # serial pass: one frame in flight on context 0; its HIP events give the kernel duration
+    elapsed_serial = timed(1, args.steps, 1) if P > 1 else elapsed
     kt = ctx.kernel_times(args.steps)
     k_ms = float(np.mean(kt)) if len(kt) else float("nan")
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     ms_per_step = elapsed / args.steps * 1e3
     value = tot["segments"] * args.steps / elapsed / 1e6
+    serial = dict(frames_in_flight=1, ms_per_frame=round(elapsed_serial / args.steps * 1e3, 4),
+                  value=round(tot["segments"] * args.steps / elapsed_serial / 1e6, 3), unit="Mrays/s")
     achieved = local_bytes / (k_ms * 1e-3) / 1e9 if k_ms == k_ms and k_ms > 0 else None
     roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=(achieved / HBM_PEAK_GBS) if achieved else None, traffic=None,
@@ -298,15 +326,18 @@ def main():
             "config": {"workload": args.config, "scene": spec.name, "width": W, "height": H, "refmax": refmax,
                        "entities": int(len(spec.entities)), "octree_nodes": int(scene.n_nodes),
                        "segments_per_frame": tot["segments"], "parallelism": "rows%d/stripe%d" % (world, args.stripe),
+                       "frames_in_flight": P, "inflight_frames_identical": same,
                        "counters": tot, "scene_build_s": round(build_s, 3)},
             "roofline": roofline,
+            "serial": serial,
             "cpu_baseline": cpu,
             "pcie_inclusive": host,
             "exposure": exposure,
             "mpixels_per_s": round(W * H * args.steps / elapsed / 1e6, 3),
         }
         print(json.dumps(rec), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 
