@@ -191,10 +191,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RT_BENCH_BACKEND") == "gloo":
+        local %= torch.cuda.device_count()       # plumbing check: ranks may share the box's one GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("RT_BENCH_BACKEND", "nccl")   # "gloo": plumbing checks with ranks sharing a GPU
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     factory, W, H, refmax = scenes.WORKLOADS[args.config]
     spec = factory()
@@ -262,6 +265,13 @@ def main():
     # every in-flight slot rendered the same camera: their gathered frames must agree bit for bit
     same = all(torch.equal(sgs[i].frame.view(torch.int32), sgs[0].frame.view(torch.int32)) for i in range(1, P)) \
         if rank == 0 else None
+    # N > 1: rank 0's gathered frame equals the whole frame rendered on its own GPU alone
+    if world > 1 and rank == 0:
+        whole = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize(dev)
+        ctx.trace_rows_device(cam, cfg, 0, 1, H, whole.data_ptr(), sp)
+        torch.cuda.synchronize(dev)
+        same = bool(same) and torch.equal(whole.view(torch.int32), sgs[0].frame.view(torch.int32))
     # serial pass: one frame in flight on context 0; its HIP events give the kernel duration
     elapsed_serial = timed(1, args.steps, 1) if P > 1 else elapsed
     kt = ctx.kernel_times(args.steps)
@@ -326,7 +336,7 @@ def main():
             "config": {"workload": args.config, "scene": spec.name, "width": W, "height": H, "refmax": refmax,
                        "entities": int(len(spec.entities)), "octree_nodes": int(scene.n_nodes),
                        "segments_per_frame": tot["segments"], "parallelism": "rows%d/stripe%d" % (world, args.stripe),
-                       "frames_in_flight": P, "inflight_frames_identical": same,
+                       "frames_in_flight": P, "frames_identical": same,
                        "counters": tot, "scene_build_s": round(build_s, 3)},
             "roofline": roofline,
             "serial": serial,
