@@ -73,10 +73,17 @@ def cpu_baseline(spec, cam, cfg, budget_s):
         segs += r["counters"]["segments"]
         done += len(pix)
         chunk = min(chunk * 2, 65536) if t_used < budget_s / 4 else chunk
+    # the same sample split over the host's CPU share (a worker split across all cores)
+    nt = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    t0 = time.perf_counter()
+    r = w.trace_frame(root, cam, cfg, pixels=order[:done], nthreads=nt)
+    t_mt = time.perf_counter() - t0
     w.close()
     return dict(value=segs / t_used / 1e6, unit="Mrays/s", cores=1, kind="port",
                 sample="%d random pixels of the %dx%d frame (%d segments) in %.1f s, oracle/rt_oracle.c, 1 thread"
-                       % (done, cam.width, cam.height, segs, t_used))
+                       % (done, cam.width, cam.height, segs, t_used),
+                threaded=dict(value=r["counters"]["segments"] / t_mt / 1e6, unit="Mrays/s", cores=nt,
+                              sample="the same pixels, %d threads, %.2f s" % (nt, t_mt)))
 
 
 TRACE_KERNELS = ("k_walk", "k_first", "k_shade", "k_cont", "k_trace")

@@ -232,7 +232,36 @@ def small_random(seed, n_tri=200, n_sph=40, n_box=10, depth=5, p_mirror=0.3, p_l
     return SceneSpec("small%d" % seed, ents, shades)
 
 
-SCENES = {"config1": config1_spheres, "config2": config2, "config3": config3}
+def config5(n_tri=1_000_000, n_sph=2000, seed=42):
+    """Config 5: 1M triangles (half-extent 0.0003) + spheres (d U[0.002,0.01]) + 16 large spheres
+    (8 glass, 8 mirrors; d U[0.08,0.2]), depth 10, refmax 5.
+    Materials ~70% matte / 25% mirror / 5% light; every third small sphere and 8 large ones are GLASS
+    with a TRANSMISSION material (refract_ray + entity_at_pos, src/raytracer.ts:135-150,238-249;
+    src/octree_entity.ts:191-202).  "Shadow rays" in BASELINE's wording have no counterpart in the
+    reference's Ray.trace (src/raytracer.ts:168-277 never samples lights), so the drop-in does not
+    add them."""
+    st = Stream(seed)
+    tri = random_triangles(st, n_tri, 0.0003, max_in_depth=10)
+    sph = random_spheres(st, n_sph, 0.002, 0.01, max_in_depth=10)
+    big = random_spheres(st, 16, 0.08, 0.2, lo=0.15, hi=0.85, max_in_depth=10)   # multi-bounce paths
+    ents = np.concatenate([tri, sph, big])
+    ents["shade"] = np.arange(len(ents))
+    shades = _materials(st, len(ents), 0.25, 0.05)
+    nb = n_tri + n_sph
+    shades["mirror"][nb + 8:], shades["light"][nb + 8:] = 1, 0
+    shades["rgb"][nb + 8:] = 0.9
+    glass = np.concatenate([n_tri + np.arange(0, n_sph, 3), nb + np.arange(8)])
+    shades["response"][glass] = abi.RT_RESP_TRANSMISSION
+    shades["mirror"][glass] = 0
+    shades["light"][glass] = 0
+    shades["rgb"][glass] = 0.9 + 0.1 * st.take(len(glass) * 3).reshape(-1, 3)
+    ents["substance"][glass] = 2                                 # GLASS (src/substance.ts:11)
+    rb, rs = room_box()
+    ents, shades = _concat([ents, rb], [shades, rs])
+    return SceneSpec("config5_1m_tri_%d_sph_glass" % n_sph, ents, shades)
+
+
+SCENES = {"config1": config1_spheres, "config2": config2, "config3": config3, "config5": config5}
 
 
 # --- camera (src/view/camera.ts:61-145) ----------------------------------------------------------
@@ -295,4 +324,6 @@ WORKLOADS = {
     "config1": (config1_spheres, 256, 256, 2),
     "config2": (config2, 1920, 1080, 1),
     "config3": (config3, 1920, 1080, 2),
+    "config4": (config3, 3840, 2160, 2),      # the 8-GPU tile-split configuration (any N runs it)
+    "config5": (config5, 3840, 2160, 5),
 }

@@ -297,7 +297,7 @@ def _sample(W, H, n, seed):
     return np.unique(np.concatenate([pix, rows]))
 
 
-@pytest.mark.parametrize("name", ["config2", "config3"])
+@pytest.mark.parametrize("name", ["config2", "config3", "config4", "config5"])
 def test_baseline_config_sampled(ctx, name):
     factory, W, H, refmax = scenes.WORKLOADS[name]
     spec = factory()
@@ -311,3 +311,6 @@ def test_baseline_config_sampled(ctx, name):
     # size-independent properties on the full frame
     assert np.all(got["status"] <= 1)
     assert np.all((got["hit_entity"] >= -1) & (got["hit_entity"] < len(spec.entities)))
+    if name == "config5":                                    # glass + mirrors: multi-bounce paths
+        assert st.segments > st.primary * 1.02
+        assert ref["counters"]["segments"] > len(pix) * 1.02
