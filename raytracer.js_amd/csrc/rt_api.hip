@@ -77,6 +77,7 @@ struct rt_ctx {
     int shade_occ = 3;               // k_shade occupancy variant (RT_SHADE_OCC)
     int cont_group = 8;              // continuation rays per wave (RT_CONT_GROUP): their passes are
                                      // latency-bound, fewer lanes per wave shorten the slowest wave
+    int seg = 1;                     // segmented walks for bounce levels >= 1 (RT_SEG=0: off)
     int occ = 0;
     int diag = 0;
     hipStream_t stream = nullptr;
@@ -120,6 +121,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_CLAIM_CHUNK")) c->claim_chunk = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_SPLIT_LEVELS")) c->split_levels = atoi(e) < 1 ? 1 : atoi(e);
     if (const char *e = getenv("RT_CONT_GROUP")) c->cont_group = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
+    if (const char *e = getenv("RT_SEG")) c->seg = atoi(e) != 0;
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     int r = use_device(c);
@@ -239,15 +241,17 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.claim_chunk = c->claim_chunk;
     L.xcd_mask = c->xcd_mask;
     L.shade_occ = c->shade_occ;
+    L.seg = c->seg;
     if (c->split && P > 0) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).
         L.cand_cap = c->cand_cap;
         if (c->b_cand.ensure(sizeof(int32_t) * (size_t)L.cand_cap * P) == RT_OK &&
-            c->b_cand_n.ensure(sizeof(int32_t) * P) == RT_OK && c->b_first.ensure(2 * sizeof(int32_t) * P) == RT_OK &&
+            c->b_cand_n.ensure(2 * sizeof(int32_t) * P) == RT_OK && c->b_first.ensure(2 * sizeof(int32_t) * P) == RT_OK &&
             c->b_queue.ensure(3 * sizeof(RtCont) * P) == RT_OK) {
             L.cand = (int32_t *)c->b_cand.p;
             L.cand_n = (int32_t *)c->b_cand_n.p;
+            L.ray_cn = L.cand_n + P;
             L.first = (int32_t *)c->b_first.p;
             L.queue[0] = (RtCont *)c->b_queue.p;
             L.queue[1] = L.queue[0] + P;

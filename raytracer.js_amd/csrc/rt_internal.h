@@ -141,6 +141,8 @@ struct RtLaunch {
     int32_t claim_chunk;                        // work items per queue claim in k_first / k_shade
     int32_t xcd_mask;                           // passes with per-XCD work bands: 1 walk, 2 first, 4 shade
     int32_t shade_occ;                          // k_shade waves per SIMD the registers must admit (3, 4, 5)
+    int32_t seg;                                // segmented walks for bounce levels >= 1 (RT_SEG; §5.10)
+    int32_t *ray_cn;                            // device [rows*W]: per-ray status of a segmented level
 };
 
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };

@@ -290,8 +290,11 @@ __device__ __forceinline__ int walker_update_next_pos(const NodeDims &p, Walker 
 
 // next — :316-361.  Returns 1 with (node, slot tree, slot octant), 0 at the end, -1 on a throw,
 // -2 at the step cap.
-template <bool INCL_UNDEF>
-__device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_tree, int &pos_oct, Counters &c)
+// STOP (segmented walks): return 2 instead of updating the empty slot
+// `stop` = tree * 8 + octant, i.e. when the walk arrives at the cell where the next segment starts.
+template <bool INCL_UNDEF, bool STOP = false>
+__device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_tree, int &pos_oct, Counters &c,
+                           int stop = -1)
 {
     while (w.cur_tree >= 0) {
         if (++c.steps > STEP_CAP) return -2;
@@ -324,6 +327,7 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
                     w.flags &= ~F_RET;
                     continue;
                 }
+                if (STOP && lnode < 0 && ltree * 8 + loct == stop) return 2;
                 if (walker_update_next_pos(node_dims(S, w.cur_tree), w, c) < 0) return -1;
             }
             if (!(w.nn & 16)) return -1;                     // vector.add(v, undefined)
@@ -1142,6 +1146,170 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
 // cand_n = count * 4 + end (0 walk finished, 1 throw, 2 step cap, 3 the continuation's
 // set_pos_and_dir threw), or -1 when the list overflowed.  The walker alone needs ~120 VGPRs
 // (4 waves/SIMD) against the fused kernel's 168 (3 waves).
+// ---- segmented continuation rays ----------------------------------------------------
+// Bounce levels >= 1 hold few rays whose walks are long chains of dependent binary64 work, so the
+// level's time is the slowest ray's chain.  Each such ray is cut into SEG_K segments along its
+// root-cube crossing, walked by SEG_K lanes at once:
+//  * segment 0 is the reference walk from the ray's origin (set_pos_and_dir, node_at_pos);
+//  * segment j >= 1 is seated in the empty slot holding the point at j/SEG_K of the crossing
+//    (node_at_pos), with the walker's origin and direction left at the ray's own;
+//  * each segment stops on arriving at the next valid segment's seat cell (walker_next<STOP>).
+// The walker's moves from an empty slot on depend only on that slot, the origin and the direction
+// (update_next_pos recomputes next_pos there), so once segment j reaches segment j+1's seat, the
+// rest of the reference walk IS segment j+1's walk.  The only difference is the walker depth: a
+// segment seated deep in the tree returns the seat's ancestors again when it climbs out of them
+// (step_back at depth 0).  Those nodes contain the seat point, so the reference returned them
+// earlier and their entities were tested; the tests are deterministic, so a re-returned node never
+// holds the first hit.  A segment that ends without reaching the next seat (walk end, throw, step
+// cap) ends the ray there, and later segments are ignored.  The concatenated lists therefore give
+// the reference's first hit (or end) exactly, whatever seats floating point produces.
+constexpr int SEG_K = 8;
+enum : int { SEG_FIN = 0, SEG_THROW = 1, SEG_CAP = 2, SEG_SEATTHROW = 3, SEG_REACHED = 4, SEG_SKIP = 5 };
+
+__device__ __forceinline__ bool seg_mode(const RtLaunch &L)
+{
+    return L.seg && L.level >= 1 &&
+           (long long)*lvl_ctr(L, L.level - 1) * SEG_K <= (long long)L.rows * (long long)L.cam.width;
+}
+
+// Walk pass, segmented: lane = (ray lane >> 3, segment lane & 7); per-segment lists at index
+// ray * SEG_K + segment, cand_n = count * 8 + SEG_* (or -1 on overflow).
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
+{
+    if (!seg_mode(L)) return;
+    const int lane = threadIdx.x & 63;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const RtDevScene &S = L.scene;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    const int n_rays = *lvl_ctr(L, L.level - 1);
+    const int items = (n_rays + 7) >> 3;
+    const int j = lane & 7;
+    for (;;) {
+        int t_end;
+        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
+        if (t >= items) break;
+        const int q = t * 8 + (lane >> 3);
+        const bool valid = q < n_rays;
+        Walker w;
+        int end = SEG_SKIP, seat = -1;
+        if (valid) {
+            const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
+            const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
+            if (j == 0) {
+                end = walker_set(S, w, o, d, false, 0, 0, c) < 0 ? SEG_SEATTHROW : SEG_FIN;
+            } else {
+                const NodeDims r = node_dims(S, 0);
+                BoxIsect bi;
+                if (box_isect(r.x + 0.5 * r.s, r.y + 0.5 * r.s, r.z + 0.5 * r.s, r.s, o, d, bi)) {
+                    const double t0 = bi.u1 > 0 ? bi.u1 : 0.0, t1 = bi.u2;
+                    if (t1 > t0 && t1 < 1e300) {
+                        const double tt = t0 + (t1 - t0) * (0.125 * j);
+                        const double x[3] = {o[0] + d[0] * tt, o[1] + d[1] * tt, o[2] + d[2] * tt};
+                        int tree = -1, oct = 0;
+                        if (node_at_pos(S, x, tree, oct, c.loc) == 1 && walker_set(S, w, o, d, true, tree, oct, c) >= 0) {
+                            seat = tree * 8 + oct;
+                            end = SEG_FIN;
+                        }
+                    }
+                }
+            }
+        }
+        // the stop cell: the seat of the next segment of this ray that has one
+        int stop = -1;
+#pragma unroll
+        for (int k = 1; k < SEG_K; k++) {
+            const int s = __shfl(seat, (lane & ~7) | (j + k < SEG_K ? j + k : SEG_K - 1), 64);
+            if (stop < 0 && j + k < SEG_K && s >= 0) stop = s;
+        }
+        int n = 0;
+        if (end == SEG_FIN) {
+            const RayBox rb = make_raybox(w.o, w.d);
+            const size_t id = (size_t)q * SEG_K + j;
+            for (;;) {
+                int node, pt, po;
+                const int r = walker_next<false, true>(S, w, node, pt, po, c, stop);
+                if (r < 0) { end = r == -2 ? SEG_CAP : SEG_THROW; break; }
+                if (r == 0) break;
+                if (r == 2) { end = SEG_REACHED; break; }
+                const RtNode &nd = S.node[node];
+                if (nd.n_ent == 0) continue;
+                if (L.cull && rb.ok && !ray_box(nd.box, rb)) continue;
+                if (n < L.cand_cap) L.cand[(size_t)n * stride + id] = node;
+                n++;
+            }
+        }
+        if (valid) L.cand_n[(size_t)q * SEG_K + j] = n > L.cand_cap ? -1 : n * 8 + end;
+    }
+}
+
+// First-hit pass, segmented: each lane scans its segment's list if every earlier segment of the
+// ray reached its successor; lane 0 of the ray's group then takes the segments in order.  Writes
+// first[ray] and ray_cn[ray] (the unsegmented cand_n convention k_shade reads: -1 overflow, else
+// end status in the low 2 bits).
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
+{
+    if (!seg_mode(L)) return;
+    const int lane = threadIdx.x & 63;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const RtDevScene &S = L.scene;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    const bool fault = L.setup->fault != 0;
+    const int n_rays = *lvl_ctr(L, L.level - 1);
+    const int items = (n_rays + 7) >> 3;
+    const int j = lane & 7, base = lane & ~7;
+    for (;;) {
+        int t_end;
+        const int t = claim_xcd(pass_heads(L, L.level, 2), items, lane, 1, t_end, L.xcd_mask & 2);
+        if (t >= items) break;
+        const int q = t * 8 + (lane >> 3);
+        const bool valid = q < n_rays;
+        const size_t id = (size_t)q * SEG_K + j;
+        const int cn = valid ? L.cand_n[id] : SEG_SKIP;
+        bool open = true;                   // all earlier segments reached their successor
+#pragma unroll
+        for (int k = 0; k < SEG_K - 1; k++) {
+            const int s = __shfl(cn, base | k, 64);
+            if (k < j && !(s >= 0 && ((s & 7) == SEG_REACHED || (s & 7) == SEG_SKIP))) open = false;
+        }
+        int2 res = make_int2(-1, -1);
+        if (valid && open && cn >= 8 && !fault) {
+            const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
+            const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
+            const RayBox rb = make_raybox(o, d);
+            const int n = cn >> 3;
+            for (int k = 0; k < n; k++) {
+                const int node = L.cand[(size_t)k * stride + id];
+                const RtNode &nd = S.node[node];
+                const int4 ent = make_int4(nd.ent_begin, nd.n_ent, nd.bvh_root, 0);
+                Hit h;
+                int rank;
+                long long box = 0;
+                const int hk = node_first_hit<false>(S, ent, o, d, rb, L.cull != 0, c, box, h, rank, true);
+                if (hk >= 0) { res = make_int2(node, hk); break; }
+            }
+        }
+        // in segment order: overflow -> the whole ray to k_cont; a hit wins; an end ends the ray
+        bool done = false;
+        int2 out = make_int2(-1, -1);
+        int ocn = 0;
+#pragma unroll
+        for (int k = 0; k < SEG_K; k++) {
+            const int s = __shfl(cn, base | k, 64);
+            const int rx = __shfl(res.x, base | k, 64), ry = __shfl(res.y, base | k, 64);
+            if (done) continue;
+            if (s < 0) { done = true; ocn = -1; }
+            else if (ry >= 0) { done = true; out = make_int2(rx, ry); ocn = 4; }
+            else if ((s & 7) != SEG_REACHED && (s & 7) != SEG_SKIP) { done = true; ocn = s & 3; }
+        }
+        if (valid && j == 0) {
+            reinterpret_cast<int2 *>(L.first)[q] = out;
+            L.ray_cn[q] = ocn;
+        }
+    }
+}
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
 {
@@ -1151,6 +1319,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (seg_mode(L)) return;                          // k_walk_seg takes this level
     for (;;) {
         int t_end;
         const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
@@ -1197,6 +1366,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const bool fault = L.setup->fault != 0;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (seg_mode(L)) return;                          // k_first_seg takes this level
     const int ch = L.claim_chunk;
     for (;;) {
         int t_end;
@@ -1238,6 +1408,7 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const RayQueues Q = {L.queue[L.level & 1], lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
     const int ch = L.claim_chunk;
+    const int32_t *ray_cn = seg_mode(L) ? L.ray_cn : L.cand_n;     // segmented levels: k_first's combined status
     for (;;) {
         int t_end;
         const int t0 = claim_xcd(pass_heads(L, L.level, 3), items, lane, ch, t_end, L.xcd_mask & 4);
@@ -1252,7 +1423,7 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
             write_pixel(L, (size_t)src.pix, R);
             continue;
         }
-        const int cn = L.cand_n[src.id];
+        const int cn = ray_cn[src.id];
         if (cn < 0) {
             // the candidate list overflowed: the fused kernel traces this ray (from its segment start)
             if (src.rec) {
@@ -1383,8 +1554,10 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             Lv.last_level = lv == levels && levels < want;
             launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lv);
             HIP_TRY(hipGetLastError());
+            if (lv >= 1 && L.seg) launch_persistent(k_walk_seg<2>, st, Lv);     // one of the two runs (§5.10)
             launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv);
             HIP_TRY(hipGetLastError());
+            if (lv >= 1 && L.seg) launch_persistent(k_first_seg<4>, st, Lv);
             launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv);
             HIP_TRY(hipGetLastError());
         }

@@ -279,6 +279,52 @@ def test_split_equals_fused(ctx, name, monkeypatch):
             c.close()
 
 
+def _transmission_spec():
+    spec = scenes.small_random(5)
+    sh = spec.shades.copy()
+    sh["response"][::3] = abi.RT_RESP_TRANSMISSION
+    sh["light"][::3] = 0
+    ents = spec.entities.copy()
+    ents["substance"][::2] = 2          # GLASS
+    ents["substance"][1::7] = -1        # undefined substance: refraction from it throws
+    return scenes.SceneSpec("transmission", ents, sh)
+
+
+@pytest.mark.parametrize("name", ["config1", "small3", "small8", "transmission", "config2"])
+@pytest.mark.parametrize("cap", [None, "2"])
+def test_segmented_equals_unsegmented(ctx, name, cap, monkeypatch):
+    """Segmented continuation walks (8 lanes per bounce ray, each walking one
+    stretch of its root crossing) change scheduling, not results: identical frames against RT_SEG=0
+    and the oracle at refmax 5, also when segment lists overflow (RT_CAND_CAP=2)."""
+    spec = {"config1": scenes.config1_spheres, "small3": lambda: scenes.small_random(3),
+            "small8": lambda: scenes.small_random(8, n_tri=800, half=0.04),
+            "transmission": _transmission_spec, "config2": scenes.config2}[name]()
+    W, H = (320, 200) if name != "transmission" else (128, 128)
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(5)
+    scene = rtamd.build_scene(spec)
+    if cap:
+        monkeypatch.setenv("RT_CAND_CAP", cap)
+    ctxs = []
+    try:
+        seg = rtamd.Context(0)
+        ctxs.append(seg)
+        seg.upload(scene)
+        a = seg.trace_frame(cam, cfg, stats=False, allow_fault=True)
+        st = seg.trace_frame(cam, cfg, allow_fault=True)["stats"]
+        # every bounce level has at most W*H/8 rays, so every level >= 1 ran segmented
+        assert 0 < (st.segments - st.primary) * 8 <= W * H
+        monkeypatch.setenv("RT_SEG", "0")
+        flat = rtamd.Context(0)
+        ctxs.append(flat)
+        flat.upload(scene)
+        _same_frames(a, flat.trace_frame(cam, cfg, stats=False, allow_fault=True))
+    finally:
+        for c in ctxs:
+            c.close()
+    w, root = oracle.build_scene(spec)
+    _compare(w.trace_frame(root, cam, cfg, nthreads=8), a)
+
+
 def test_roughness_rejected(ctx):
     spec = scenes.config1_spheres()
     sh = spec.shades.copy()
