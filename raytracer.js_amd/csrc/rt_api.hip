@@ -77,7 +77,7 @@ struct rt_ctx {
     int shade_occ = 3;               // k_shade occupancy variant (RT_SHADE_OCC)
     int cont_group = 8;              // continuation rays per wave (RT_CONT_GROUP): their passes are
                                      // latency-bound, fewer lanes per wave shorten the slowest wave
-    int seg = 1;                     // segmented walks for bounce levels >= 1 (RT_SEG=0: off)
+    int seg = 8;                     // segments per bounce ray, levels >= 1 (RT_SEG: 0/1 off, 2..64)
     int occ = 0;
     int diag = 0;
     hipStream_t stream = nullptr;
@@ -85,7 +85,7 @@ struct rt_ctx {
     bool scatter = false;            // a mirror shade with roughness > 0 is reachable
     RtDevScene scene{};
     RtSceneStore *store = nullptr;   // the resident scene (rt_scene.hip)
-    DevBuf b_stat, b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_fr, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
+    DevBuf b_stat, b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
     DevBuf b_walk;
     static constexpr int NEV = 256;
     hipEvent_t ev[NEV][2] = {};
@@ -121,7 +121,11 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_CLAIM_CHUNK")) c->claim_chunk = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_SPLIT_LEVELS")) c->split_levels = atoi(e) < 1 ? 1 : atoi(e);
     if (const char *e = getenv("RT_CONT_GROUP")) c->cont_group = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
-    if (const char *e = getenv("RT_SEG")) c->seg = atoi(e) != 0;
+    if (const char *e = getenv("RT_SEG")) {
+        int k = 1;
+        while (k < 64 && 2 * k <= atoi(e)) k *= 2;                  // a power of two, at most 64
+        c->seg = atoi(e) > 1 ? k : 0;
+    }
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     int r = use_device(c);
@@ -150,7 +154,7 @@ extern "C" void rt_destroy(rt_ctx *c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     rt_store_free(c->store);
     c->store = nullptr;
-    DevBuf *bufs[] = {&c->b_stat, &c->b_cand, &c->b_cand_n, &c->b_first, &c->b_queue, &c->b_ctr, &c->b_setup, &c->b_fr, &c->b_dirs,
+    DevBuf *bufs[] = {&c->b_stat, &c->b_cand, &c->b_cand_n, &c->b_first, &c->b_queue, &c->b_ctr, &c->b_setup, &c->b_dirs,
                       &c->b_rgb, &c->b_hit_e, &c->b_hit_n, &c->b_status, &c->b_counters, &c->b_fault,
                       &c->b_walk};
     for (DevBuf *b : bufs) b->release();
@@ -210,7 +214,6 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     const int rows = rt_part_rows(cam->height, part, n_parts, stripe);
     const size_t P = (size_t)rows * (size_t)cam->width;
     int r;
-    if ((r = c->b_fr.ensure(sizeof(double) * 3 * (size_t)cam->height)) != RT_OK) return r;
     if ((r = c->b_dirs.ensure(sizeof(double) * 3 * (P ? P : 1))) != RT_OK) return r;
     if (want_ids) {
         if ((r = c->b_hit_e.ensure(sizeof(int32_t) * (P ? P : 1))) != RT_OK) return r;
@@ -226,7 +229,6 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.stripe_rows = stripe;
     L.rows = rows;
     L.setup = (RtFrameSetup *)c->b_setup.p;
-    L.fr_rows = (double *)c->b_fr.p;
     L.dirs = (double *)c->b_dirs.p;
     L.hit_entity = want_ids ? (int32_t *)c->b_hit_e.p : nullptr;
     L.hit_node = want_ids ? (int32_t *)c->b_hit_n.p : nullptr;

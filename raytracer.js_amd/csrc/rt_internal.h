@@ -115,7 +115,6 @@ struct RtLaunch {
     rt_config_desc cfg;
     int32_t part, n_parts, stripe_rows, rows;   // this part's row set
     RtFrameSetup *setup;                        // device
-    double *fr_rows;                            // device [H*3]
     double *dirs;                               // device [3][rows*W] (SoA planes)
     float *rgb;                                 // device [rows*W*3]
     int32_t *hit_entity, *hit_node;             // device [rows*W] or null
@@ -141,7 +140,7 @@ struct RtLaunch {
     int32_t claim_chunk;                        // work items per queue claim in k_first / k_shade
     int32_t xcd_mask;                           // passes with per-XCD work bands: 1 walk, 2 first, 4 shade
     int32_t shade_occ;                          // k_shade waves per SIMD the registers must admit (3, 4, 5)
-    int32_t seg;                                // segmented walks for bounce levels >= 1 (RT_SEG; §5.10)
+    int32_t seg;                                // segments per bounce ray, levels >= 1 (0: off; RT_SEG; §5.10)
     int32_t *ray_cn;                            // device [rows*W]: per-ray status of a segmented level
 };
 

@@ -1,8 +1,8 @@
 // rt_kernels.hip — gfx950 kernels of the raytracer.js render path.
 //
-//   k_frame_setup   once per frame: start node / start substance (src/raytracer.ts:309-313) and the
-//                   vertical scan chains of Camera.get_dir_for_each_pixel (src/view/camera.ts:231-249)
-//   k_raygen        one lane per half-row: the horizontal scan chains (src/view/camera.ts:215-229)
+//   k_frame_start   once per frame: start node / start substance (src/raytracer.ts:309-313), and
+//                   the ray directions: Camera.get_dir_for_each_pixel's vertical and horizontal
+//                   scan chains (src/view/camera.ts:207-250), one lane per component x half-row
 //   k_trace         one lane per pixel: Ray.trace (src/raytracer.ts:168-277) over the linearised
 //                   octree with the OctreeWalker visit order (src/octree_space.ts:316-361), entity
 //                   tests (src/entities/*), SolidMaterial shading, sky / inverse-square law, and the
@@ -581,16 +581,6 @@ __device__ int node_first_hit(const RtDevScene &S, const int4 ne, const double o
 }
 
 // ---- camera scan (src/view/camera.ts:207-250; vector.rotate_vectors src/math/vector.ts:318-323) ----
-__device__ __forceinline__ void rotate_pair(double bx[3], double by[3], double c, double s)
-{
-    double nx[3], ny[3];
-    for (int i = 0; i < 3; i++) {
-        nx[i] = bx[i] * c + by[i] * s;
-        ny[i] = bx[i] * -s + by[i] * c;
-    }
-    for (int i = 0; i < 3; i++) { bx[i] = nx[i]; by[i] = ny[i]; }
-}
-
 __device__ __forceinline__ int part_row_to_y(int lr, int part, int n_parts, int stripe)
 {
     const int k = lr / stripe;
@@ -605,15 +595,32 @@ __device__ __forceinline__ int wave_min(int v)
     return v;
 }
 
-// Two waves: wave 0 runs the two vertical scan chains (lanes 0/1); wave 1 locates the camera
-// (node_at_pos) and finds its substance with a wave-cooperative entity_at_pos (64 entities per
-// step, minimum Set rank among is_within hits).
-__global__ void __launch_bounds__(128) k_frame_setup(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
-                                                     RtFrameSetup *setup, double *fr_rows)
+// Frame start, one launch: block 0's first wave locates the camera (node_at_pos) and finds its
+// substance with a wave-cooperative entity_at_pos (64 entities per step, minimum Set rank among
+// is_within hits); the other blocks generate the ray directions.
+//
+// Camera.get_dir_for_each_pixel is two nested chains of incremental rotations: the vertical chain
+// gives each row its centre direction (iter_v), the row's horizontal chain then its pixels
+// (iter_h).  rotate_vectors works component by component (x' = x c + y s, y' = -x s + y c), so
+// each of the 3 components is an independent 2-term recurrence.  One lane per (component, half,
+// row) runs its row's vertical chain and then the half-row: 6 * rows lanes whose critical path is
+// at most H/2 + W/2 steps of one multiply-add pair, bit-identical to the sequential scan.
+// dirs: SoA planes [3][W*rows], x-major (index x*rows + local row): a wave stores 64 consecutive
+// rows of one column per step, and an 8x8 tile of the walk reads 8 runs of 64 bytes per plane.
+__device__ __forceinline__ void rotate_1(double &x, double &y, double c, double s)
+{
+    const double nx = x * c + y * s, ny = x * -s + y * c;      // rotate_vectors, one component
+    x = nx;
+    y = ny;
+}
+
+__global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
+                                                     RtFrameSetup *setup, int part, int n_parts, int stripe,
+                                                     int rows, double *__restrict__ dirs)
 {
     const int lane = threadIdx.x & 63;
-    const int H = cam.height;
-    if (threadIdx.x >= 64) {
+    if (blockIdx.x == 0) {
+        if (threadIdx.x >= 64) return;
         long long lv = 0;
         int t = -1, oc = 0;
         const int r = node_at_pos(S, cam.pos, t, oc, lv);
@@ -638,48 +645,34 @@ __global__ void __launch_bounds__(128) k_frame_setup(RtDevScene S, rt_camera_des
         }
         return;
     }
-    if (lane == 0 || lane == 1) {
-        // iter_v(H>>1, H, rot_scan_v_v, 1, false) / iter_v((H>>1)-1, -1, counter, -1, true)
-        const bool top = lane == 0;
-        const double c = cam.scan_v[0], s = top ? cam.scan_v[1] : -cam.scan_v[1];
-        double fr[3] = {cam.fr[0], cam.fr[1], cam.fr[2]}, up[3] = {cam.up[0], cam.up[1], cam.up[2]};
-        if (!top) rotate_pair(fr, up, c, s);
-        const int from = top ? (H >> 1) : (H >> 1) - 1, to = top ? H : -1, inc = top ? 1 : -1;
-        for (int y = from; y != to; y += inc) {
-            fr_rows[3 * y + 0] = fr[0];
-            fr_rows[3 * y + 1] = fr[1];
-            fr_rows[3 * y + 2] = fr[2];
-            rotate_pair(fr, up, c, s);
-        }
-    }
-}
-
-// One lane per (half, row of this part): lanes [0, rows) run the right half-rows, [rows, 2 rows)
-// the left ones, so at every chain step a wave stores 64 consecutive rows of one column.
-// dirs: SoA planes [3][W*rows], x-major (index x*rows + local row): coalesced stores here, and
-// an 8x8 tile of k_trace reads 8 runs of 64 bytes per plane.
-__global__ void __launch_bounds__(256) k_raygen(rt_camera_desc cam, int part, int n_parts, int stripe, int rows,
-                                                const double *__restrict__ fr_rows, double *__restrict__ dirs)
-{
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 2 * rows) return;
-    const bool right = t < rows;
-    const int lr = right ? t : t - rows;
-    const int W = cam.width;
+    const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
+    if (t >= 6 * rows) return;
+    const int lr = t % rows, hc = t / rows;
+    const int i = hc >> 1;                    // component
+    const bool right = (hc & 1) == 0;
+    const int W = cam.width, H = cam.height;
     const int y = part_row_to_y(lr, part, n_parts, stripe);
+    // iter_v(H>>1, H, rot_scan_v_v, 1, false) / iter_v((H>>1)-1, -1, counter, -1, true): the row's
+    // direction is fr after y - H/2 rotations (top), or after the counter pre-rotation and
+    // H/2 - 1 - y more (bottom)
+    double f = cam.fr[i], u = cam.up[i];
+    {
+        const double c = cam.scan_v[0];
+        const bool top = y >= (H >> 1);
+        const double sv = top ? cam.scan_v[1] : -cam.scan_v[1];
+        if (!top) rotate_1(f, u, c, sv);
+        const int steps = top ? y - (H >> 1) : (H >> 1) - 1 - y;
+        for (int k = 0; k < steps; k++) rotate_1(f, u, c, sv);
+    }
     // iter_h(W>>1, W, y, rot_scan_h_v, fr_v, 1, false) / iter_h((W>>1)-1, -1, y, counter, fr_v, -1, true)
-    const double c = cam.scan_h[0], s = right ? cam.scan_h[1] : -cam.scan_h[1];
-    double f[3] = {fr_rows[3 * y], fr_rows[3 * y + 1], fr_rows[3 * y + 2]};
-    double l[3] = {cam.lf[0], cam.lf[1], cam.lf[2]};
-    if (!right) rotate_pair(f, l, c, s);
+    const double c = cam.scan_h[0], sh = right ? cam.scan_h[1] : -cam.scan_h[1];
+    double l = cam.lf[i];
+    if (!right) rotate_1(f, l, c, sh);
     const int from = right ? (W >> 1) : (W >> 1) - 1, to = right ? W : -1, inc = right ? 1 : -1;
-    const size_t plane = (size_t)rows * (size_t)W;
+    double *plane = dirs + (size_t)i * (size_t)rows * (size_t)W;
     for (int x = from; x != to; x += inc) {
-        const size_t i = (size_t)x * (size_t)rows + (size_t)lr;
-        dirs[i] = f[0];
-        dirs[plane + i] = f[1];
-        dirs[2 * plane + i] = f[2];
-        rotate_pair(f, l, c, s);
+        plane[(size_t)x * (size_t)rows + (size_t)lr] = f;
+        rotate_1(f, l, c, sh);
     }
 }
 
@@ -1071,7 +1064,7 @@ __device__ __forceinline__ void ray_src(const RtLaunch &L, int item, int lane, R
         r.id = (size_t)lr * (size_t)W + (size_t)x;
         r.pix = (int)r.id;
         const size_t plane = (size_t)L.rows * (size_t)W;
-        const size_t di = (size_t)x * (size_t)L.rows + (size_t)lr;           // x-major (k_raygen)
+        const size_t di = (size_t)x * (size_t)L.rows + (size_t)lr;           // x-major (k_frame_start)
         for (int i = 0; i < 3; i++) { r.o[i] = L.cam.pos[i]; r.d[i] = L.dirs[(size_t)i * plane + di]; }
     } else {
         const int q = item * L.cont_group + lane;
@@ -1148,10 +1141,10 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
 // (4 waves/SIMD) against the fused kernel's 168 (3 waves).
 // ---- segmented continuation rays ----------------------------------------------------
 // Bounce levels >= 1 hold few rays whose walks are long chains of dependent binary64 work, so the
-// level's time is the slowest ray's chain.  Each such ray is cut into SEG_K segments along its
-// root-cube crossing, walked by SEG_K lanes at once:
+// level's time is the slowest ray's chain.  Each such ray is cut into K segments along its
+// root-cube crossing, walked by K lanes at once (K = L.seg, RT_SEG):
 //  * segment 0 is the reference walk from the ray's origin (set_pos_and_dir, node_at_pos);
-//  * segment j >= 1 is seated in the empty slot holding the point at j/SEG_K of the crossing
+//  * segment j >= 1 is seated in the empty slot holding the point at j/K of the crossing
 //    (node_at_pos), with the walker's origin and direction left at the ray's own;
 //  * each segment stops on arriving at the next valid segment's seat cell (walker_next<STOP>).
 // The walker's moves from an empty slot on depend only on that slot, the origin and the direction
@@ -1163,17 +1156,17 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
 // holds the first hit.  A segment that ends without reaching the next seat (walk end, throw, step
 // cap) ends the ray there, and later segments are ignored.  The concatenated lists therefore give
 // the reference's first hit (or end) exactly, whatever seats floating point produces.
-constexpr int SEG_K = 8;
+// segments per ray: L.seg (a power of two <= 64), default 8
 enum : int { SEG_FIN = 0, SEG_THROW = 1, SEG_CAP = 2, SEG_SEATTHROW = 3, SEG_REACHED = 4, SEG_SKIP = 5 };
 
 __device__ __forceinline__ bool seg_mode(const RtLaunch &L)
 {
-    return L.seg && L.level >= 1 &&
-           (long long)*lvl_ctr(L, L.level - 1) * SEG_K <= (long long)L.rows * (long long)L.cam.width;
+    return L.seg > 1 && L.level >= 1 &&
+           (long long)*lvl_ctr(L, L.level - 1) * L.seg <= (long long)L.rows * (long long)L.cam.width;
 }
 
-// Walk pass, segmented: lane = (ray lane >> 3, segment lane & 7); per-segment lists at index
-// ray * SEG_K + segment, cand_n = count * 8 + SEG_* (or -1 on overflow).
+// Walk pass, segmented: K = L.seg lanes per ray, lane = (ray lane / K, segment lane % K);
+// per-segment lists at index ray * K + segment, cand_n = count * 8 + SEG_* (or -1 on overflow).
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
 {
@@ -1183,13 +1176,15 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const int n_rays = *lvl_ctr(L, L.level - 1);
-    const int items = (n_rays + 7) >> 3;
-    const int j = lane & 7;
+    const int K = L.seg, rpw = 64 / K;           // segments per ray, rays per wave
+    const int items = (n_rays + rpw - 1) / rpw;
+    const int j = lane & (K - 1), base = lane & ~(K - 1);
+    const double frac = (double)j / (double)K;
     for (;;) {
         int t_end;
         const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
         if (t >= items) break;
-        const int q = t * 8 + (lane >> 3);
+        const int q = t * rpw + lane / K;
         const bool valid = q < n_rays;
         Walker w;
         int end = SEG_SKIP, seat = -1;
@@ -1204,7 +1199,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
                 if (box_isect(r.x + 0.5 * r.s, r.y + 0.5 * r.s, r.z + 0.5 * r.s, r.s, o, d, bi)) {
                     const double t0 = bi.u1 > 0 ? bi.u1 : 0.0, t1 = bi.u2;
                     if (t1 > t0 && t1 < 1e300) {
-                        const double tt = t0 + (t1 - t0) * (0.125 * j);
+                        const double tt = t0 + (t1 - t0) * frac;
                         const double x[3] = {o[0] + d[0] * tt, o[1] + d[1] * tt, o[2] + d[2] * tt};
                         int tree = -1, oct = 0;
                         if (node_at_pos(S, x, tree, oct, c.loc) == 1 && walker_set(S, w, o, d, true, tree, oct, c) >= 0) {
@@ -1217,15 +1212,14 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
         }
         // the stop cell: the seat of the next segment of this ray that has one
         int stop = -1;
-#pragma unroll
-        for (int k = 1; k < SEG_K; k++) {
-            const int s = __shfl(seat, (lane & ~7) | (j + k < SEG_K ? j + k : SEG_K - 1), 64);
-            if (stop < 0 && j + k < SEG_K && s >= 0) stop = s;
+        for (int k = 1; k < K; k++) {
+            const int s = __shfl(seat, base | (j + k < K ? j + k : K - 1), 64);
+            if (stop < 0 && j + k < K && s >= 0) stop = s;
         }
         int n = 0;
         if (end == SEG_FIN) {
             const RayBox rb = make_raybox(w.o, w.d);
-            const size_t id = (size_t)q * SEG_K + j;
+            const size_t id = (size_t)q * K + j;
             for (;;) {
                 int node, pt, po;
                 const int r = walker_next<false, true>(S, w, node, pt, po, c, stop);
@@ -1239,7 +1233,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
                 n++;
             }
         }
-        if (valid) L.cand_n[(size_t)q * SEG_K + j] = n > L.cand_cap ? -1 : n * 8 + end;
+        if (valid) L.cand_n[(size_t)q * K + j] = n > L.cand_cap ? -1 : n * 8 + end;
     }
 }
 
@@ -1257,19 +1251,19 @@ __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const bool fault = L.setup->fault != 0;
     const int n_rays = *lvl_ctr(L, L.level - 1);
-    const int items = (n_rays + 7) >> 3;
-    const int j = lane & 7, base = lane & ~7;
+    const int K = L.seg, rpw = 64 / K;
+    const int items = (n_rays + rpw - 1) / rpw;
+    const int j = lane & (K - 1), base = lane & ~(K - 1);
     for (;;) {
         int t_end;
         const int t = claim_xcd(pass_heads(L, L.level, 2), items, lane, 1, t_end, L.xcd_mask & 2);
         if (t >= items) break;
-        const int q = t * 8 + (lane >> 3);
+        const int q = t * rpw + lane / K;
         const bool valid = q < n_rays;
-        const size_t id = (size_t)q * SEG_K + j;
+        const size_t id = (size_t)q * K + j;
         const int cn = valid ? L.cand_n[id] : SEG_SKIP;
         bool open = true;                   // all earlier segments reached their successor
-#pragma unroll
-        for (int k = 0; k < SEG_K - 1; k++) {
+        for (int k = 0; k < K - 1; k++) {
             const int s = __shfl(cn, base | k, 64);
             if (k < j && !(s >= 0 && ((s & 7) == SEG_REACHED || (s & 7) == SEG_SKIP))) open = false;
         }
@@ -1294,8 +1288,7 @@ __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
         bool done = false;
         int2 out = make_int2(-1, -1);
         int ocn = 0;
-#pragma unroll
-        for (int k = 0; k < SEG_K; k++) {
+        for (int k = 0; k < K; k++) {
             const int s = __shfl(cn, base | k, 64);
             const int rx = __shfl(res.x, base | k, 64), ry = __shfl(res.y, base | k, 64);
             if (done) continue;
@@ -1523,13 +1516,11 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
 {
     hipStream_t st = (hipStream_t)stream;
     const int W = L.cam.width;
-    hipLaunchKernelGGL(k_frame_setup, dim3(1), dim3(128), 0, st, L.scene, L.cam, L.cfg, L.setup, L.fr_rows);
+    const int rg_lanes = 6 * (L.rows > 0 ? L.rows : 0);
+    hipLaunchKernelGGL(k_frame_start, dim3(1 + (rg_lanes + 255) / 256), dim3(256), 0, st, L.scene, L.cam, L.cfg,
+                       L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.dirs);
     HIP_TRY(hipGetLastError());
     if (L.rows <= 0) return RT_OK;
-    const int rg_threads = 2 * L.rows;
-    hipLaunchKernelGGL(k_raygen, dim3((rg_threads + 255) / 256), dim3(256), 0, st, L.cam, L.part, L.n_parts,
-                       L.stripe_rows, L.rows, (const double *)L.fr_rows, L.dirs);
-    HIP_TRY(hipGetLastError());
     if (L.skip_trace) return RT_OK;
     (void)W;
     HIP_TRY(hipMemsetAsync(L.ctr, 0, sizeof(int32_t) * RT_CTR_INTS, st));
@@ -1554,10 +1545,10 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             Lv.last_level = lv == levels && levels < want;
             launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lv);
             HIP_TRY(hipGetLastError());
-            if (lv >= 1 && L.seg) launch_persistent(k_walk_seg<2>, st, Lv);     // one of the two runs (§5.10)
+            if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lv);     // one of the two runs (§5.10)
             launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv);
             HIP_TRY(hipGetLastError());
-            if (lv >= 1 && L.seg) launch_persistent(k_first_seg<4>, st, Lv);
+            if (lv >= 1 && L.seg > 1) launch_persistent(k_first_seg<4>, st, Lv);
             launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv);
             HIP_TRY(hipGetLastError());
         }
