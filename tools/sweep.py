@@ -18,7 +18,7 @@ import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
 
 KNOBS = ("RT_OCC", "RT_DIAG", "RT_NO_CULL", "RT_BVH_SAH", "RT_SPLIT", "RT_CAND_CAP", "RT_CONT_GROUP", "RT_SPLIT_LEVELS",
-         "RT_CLAIM_CHUNK", "RT_XCD", "RT_SHADE_OCC", "RT_SEG")
+         "RT_CLAIM_CHUNK", "RT_XCD", "RT_SHADE_OCC", "RT_SEG", "RT_SKIP")
 
 
 def main():
@@ -52,10 +52,10 @@ def main():
         s.synchronize()
         wall = (time.perf_counter() - t0) / a.frames * 1e3
         kt = ctx.kernel_times(a.frames)
-        extra = {}
+        extra = {"rgb_sum": int(buf.view(torch.int32).to(torch.int64).sum())}   # frame fingerprint
         if int(os.environ.get("RT_DIAG", "0")) & 8:
             tile = st.n_loc
-            extra = dict(lane_cycles_tile=tile, frac_walk=round(st.n_cull / tile, 3), frac_test=round(st.n_exact / tile, 3),
+            extra.update(lane_cycles_tile=tile, frac_walk=round(st.n_cull / tile, 3), frac_test=round(st.n_exact / tile, 3),
                          frac_other=round(1 - (st.n_cull + st.n_exact) / tile, 3))
         rec = dict(variant=name, env=kv, kernel_ms=round(float(kt.mean()), 3), kernel_min=round(float(kt.min()), 3),
                    wall_ms=round(wall, 3), mrays=round(st.segments / (wall * 1e-3) / 1e6, 2),
