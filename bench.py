@@ -4,8 +4,10 @@ A step is one frame: ray generation + trace + (N>1) RCCL gather of the row strip
 de-interleave into the 1920x1080 frame.  The frame is split across ranks (strong scaling: the
 frame size is fixed).  Inputs (scene, camera) are resident on the GPU before the timed region.
 
-Frames in flight (--inflight P, default 4): each rank keeps P contexts, each on its own HIP
-stream with its own frame buffers, and issues frame f on context f % P.  A frame's bounce level 1
+Frames in flight (--inflight P, default 16): each rank keeps P contexts, each on its own HIP
+stream with its own frame buffers, and issues frame f on context f % P.  HIP maps streams onto
+GPU_MAX_HW_QUEUES hardware queues (HIP's default is 4); the bench raises it to 16 before the HIP
+runtime starts, so that 16 frames really run concurrently.  A frame's bounce level 1
 is a latency-bound tail (few, long continuation rays) that the next frames' primary
 passes fill.  Every one of the K timed frames is rendered and gathered completely inside the timed
 region; `value` is their throughput.  A serial pass (one frame in flight) reports the per-frame
@@ -19,11 +21,17 @@ kernel (algorithmic bytes per launch from the kernel's own work counters, SURVEY
 HIP-event-timed kernel duration) and `cpu_baseline` (the oracle restatement, single-threaded, on a
 bounded pixel sample of the same workload).
 """
+import os
+
+# hardware queues for the frames in flight, read once when the HIP runtime initialises: at least
+# 16 (HIP's default, and the GPU box's setting, is 4; DESIGN.md §7)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 import argparse
 import csv
 import glob
 import json
-import os
 import shutil
 import subprocess
 import sys
@@ -183,13 +191,13 @@ def pmc_child(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="config3", choices=sorted(scenes.WORKLOADS))
     ap.add_argument("--stripe", type=int, default=8, help="rows per stripe of the row-interleaved split")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
-    ap.add_argument("--inflight", type=int, default=4, help="frames in flight per rank (contexts / streams)")
+    ap.add_argument("--inflight", type=int, default=16, help="frames in flight per rank (contexts / streams)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:

@@ -9,7 +9,7 @@ which de-interleaves them into frame order with one index_select.  No other exch
 data path.
 
 `StripeGather` holds the buffers and the row index; it works with any torch.distributed backend
-(RCCL on the GPU box, gloo for the CPU tests) and with world_size 1 (plain copy).
+(RCCL on the GPU box, gloo for the CPU tests) and with world_size 1 (the local buffer is the frame).
 """
 import numpy as np
 import torch
@@ -52,12 +52,17 @@ class StripeGather:
         src, self.max_rows = source_index(H, world, stripe)
         self.rows = len(part_rows(H, rank, world, stripe))
         self.local = torch.zeros((self.max_rows, W, channels), dtype=dtype, device=device)
-        self.frame = torch.zeros((H, W, channels), dtype=dtype, device=device) if rank == 0 else None
+        if world == 1:
+            self.frame = self.local          # one part: rows are already in frame order, nothing to move
+        else:
+            self.frame = torch.zeros((H, W, channels), dtype=dtype, device=device) if rank == 0 else None
         if world > 1 and rank == 0:
-            self._bufs = [torch.empty_like(self.local) for _ in range(world)]
+            # the ranks' buffers land in one stacked tensor (views), de-interleaved without a restack
+            self._stack = torch.empty((world,) + tuple(self.local.shape), dtype=dtype, device=device)
+            self._bufs = list(self._stack.unbind(0))
             self._src = torch.from_numpy(src).to(device)
         else:
-            self._bufs, self._src = None, None
+            self._stack, self._bufs, self._src = None, None, None
         if self.local.is_cuda:
             # the fills ran on torch's stream; rt_trace_rows_device writes `local` on another one
             torch.cuda.synchronize(self.local.device)
@@ -65,11 +70,10 @@ class StripeGather:
     def gather(self):
         """Collective (every rank calls it): rank 0's `frame` receives the whole image."""
         if self.world == 1:
-            self.frame.copy_(self.local[:self.H])
             return self.frame
         dist.gather(self.local, self._bufs if self.rank == 0 else None, dst=0)
         if self.rank == 0:
-            flat = torch.stack(self._bufs).view(self.world * self.max_rows, self.W, -1)
+            flat = self._stack.view(self.world * self.max_rows, self.W, -1)
             torch.index_select(flat, 0, self._src, out=self.frame)
             return self.frame
         return None

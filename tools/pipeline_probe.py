@@ -3,9 +3,15 @@ frames, for a part of n_parts row stripes (n_parts = 8 models one GPU of an 8-GP
 
 python tools/pipeline_probe.py [--parts 1 8] [--inflight 1 2 3] [--frames 30]
 """
+import os
+
+# hardware queues for the frames in flight, read once when the HIP runtime initialises: at least
+# 16 (HIP's default, and the GPU box's setting, is 4; DESIGN.md §7)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 import argparse
 import json
-import os
 import sys
 import time
 
