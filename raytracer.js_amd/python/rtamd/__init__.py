@@ -12,7 +12,7 @@ import numpy as np
 from . import abi
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "librt_amd.so")
+LIB_PATH = os.environ.get("RT_LIB") or os.path.join(PKG_DIR, "lib", "librt_amd.so")   # RT_LIB: A/B builds (tools)
 
 _lib = None
 

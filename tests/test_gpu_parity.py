@@ -197,6 +197,33 @@ def test_camera_outside_root(ctx):
     _compare(ref, got)
 
 
+def _placed(spec, P, s):
+    """The scene moved into the root cube [P, P + s): every coordinate x -> P + s*x, sizes * s."""
+    e = spec.entities.copy()
+    g = e["geom"]
+    P = np.asarray(P, np.float64)
+    for t in (abi.RT_ENT_SPHERE, abi.RT_ENT_BOX):
+        m = e["type"] == t
+        g[m, :3] = P + s * g[m, :3]
+        g[m, 3] *= s
+    m = e["type"] == abi.RT_ENT_FACE
+    for k in range(3):
+        g[m, 3 * k:3 * k + 3] = P + s * g[m, 3 * k:3 * k + 3]
+    return scenes.SceneSpec(spec.name + "_placed", e, spec.shades, spec.substances, tuple(P), s)
+
+
+@pytest.mark.parametrize("P,s", [((0.5, -1.5, 2.0), 3.0), ((-2.0, -2.0, 1.0), 4.0), ((0.5, 0.25, -0.125), 0.75)])
+def test_placed_roots(ctx, P, s):
+    """Roots off the unit cube.  A non-dyadic root (size 3 or 0.75, offsets not on the grid) takes
+    the walker's general path (entry checks after sibling moves); a dyadic root at
+    an offset (size 4) takes the sibling-move shortcut.  Both equal the oracle bit for bit."""
+    spec = _placed(scenes.small_random(4, n_tri=400), P, s)
+    cam = scenes.make_camera(160, 120, pos=tuple(np.asarray(P) + 0.5 * s))
+    ref, got = _run_both(ctx, spec, cam, scenes.make_config(3))
+    _compare(ref, got)
+    assert got["stats"].counters() == ref["counters"]
+
+
 def test_exposure_blend(ctx):
     """ExposureBuffer.next_frame weight 1/(1+n): c*w + old*(1-w) in f64, stored as f32."""
     spec = scenes.small_random(2)
