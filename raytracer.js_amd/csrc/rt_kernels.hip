@@ -208,34 +208,25 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
     double m = INFINITY;
 #pragma unroll
     for (int a = 0; a < 3; a++) m = ae[a] < m ? ae[a] : m;
-    double u2 = INFINITY;
-    int i2 = -1;
-    if (m < INFINITY) {
-        const double tol = fabs(m) * 1.7763568394002505e-15 + 1e-300;   // 8 eps |m| + subnormal slack
-        if (!(fabs(m) < 1e300)) {
-            // out of the shortcut's range: exact for every axis
+    const double tol = fabs(m) * 1.7763568394002505e-15 + 1e-300;   // 8 eps |m| + subnormal slack
+    const bool s0 = ae[0] <= m + tol, s1 = ae[1] <= m + tol, s2 = ae[2] <= m + tol;   // NaN never survives
+    // the common case, straight-line: one survivor of a finite minimum in the shortcut's range,
+    // selected without branching so that every lane of the wave shares one division
+    const bool common = fabs(m) < 1e300 && (int)s0 + (int)s1 + (int)s2 == 1;
+    double u2 = (s0 ? qe[0] : (s1 ? qe[1] : qe[2])) / (s0 ? pe[0] : (s1 ? pe[1] : pe[2]));
+    int i2 = s0 ? fe[0] : (s1 ? fe[1] : fe[2]);
+    if (!(u2 < INFINITY)) { u2 = INFINITY; i2 = -1; }          // (a finite survivor never gets here)
+    if (!common) {
+        // no finite exit, |m| out of the shortcut's range (every axis exact), or several survivors
+        u2 = INFINITY;
+        i2 = -1;
+        if (m < INFINITY) {
+            const bool all = !(fabs(m) < 1e300);
 #pragma unroll
             for (int a = 0; a < 3; a++) {
-                const double e = qe[a] / pe[a];
-                if (e < u2) { u2 = e; i2 = fe[a]; }
-            }
-        } else {
-            const bool s0 = ae[0] <= m + tol, s1 = ae[1] <= m + tol, s2 = ae[2] <= m + tol;   // NaN never survives
-            if ((int)s0 + (int)s1 + (int)s2 == 1) {
-                // the common case: one survivor, selected without branching so that every lane of the
-                // wave shares a single division whichever face it leaves through
-                const double q = s0 ? qe[0] : (s1 ? qe[1] : qe[2]);
-                const double pp = s0 ? pe[0] : (s1 ? pe[1] : pe[2]);
-                const int f = s0 ? fe[0] : (s1 ? fe[1] : fe[2]);
-                const double e = q / pp;
-                if (e < u2) { u2 = e; i2 = f; }
-            } else {
-#pragma unroll
-                for (int a = 0; a < 3; a++) {
-                    if (ae[a] <= m + tol) {
-                        const double e = qe[a] / pe[a];
-                        if (e < u2) { u2 = e; i2 = fe[a]; }
-                    }
+                if (all || ae[a] <= m + tol) {
+                    const double e = qe[a] / pe[a];
+                    if (e < u2) { u2 = e; i2 = fe[a]; }
                 }
             }
         }
@@ -244,17 +235,15 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
     double M = -INFINITY;
 #pragma unroll
     for (int a = 0; a < 3; a++) M = an[a] > M ? an[a] : M;
-    if (M > -INFINITY) {
-        const double tolM = fabs(M) * 1.7763568394002505e-15 + 1e-300;
-        if (!(M + tolM < u2) || !(fabs(M) < 1e300)) {
-            double u1 = -INFINITY;
+    const double tolM = fabs(M) * 1.7763568394002505e-15 + 1e-300;
+    if (M > -INFINITY && (!(M + tolM < u2) || !(fabs(M) < 1e300))) {
+        double u1 = -INFINITY;
 #pragma unroll
-            for (int a = 0; a < 3; a++) {
-                const double e = qn[a] / pn[a];
-                if (e > u1) u1 = e;
-            }
-            if (u1 > u2) return false;
+        for (int a = 0; a < 3; a++) {
+            const double e = qn[a] / pn[a];
+            if (e > u1) u1 = e;
         }
+        if (u1 > u2) return false;
     }
     u2o = u2;
     i2o = i2;
