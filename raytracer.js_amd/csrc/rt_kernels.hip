@@ -1033,10 +1033,22 @@ struct RaySrc {
     double o[3], d[3];
 };
 
+// Continuation rays per wave at a bounce level: L.cont_group (8) while the level's rays are few
+// (config 3: 21.7 k; their passes are latency-bound and narrow waves shorten the slowest one), up
+// to 64 once they would need more than ~4096 waves (config 5: millions of bounce rays, where
+// 8-lane waves leave 7/8 of every SIMD idle).  Uniform per launch: the count is final by then.
+__device__ __forceinline__ int cont_g(const RtLaunch &L)
+{
+    const int n = *lvl_ctr(L, L.level - 1);
+    int g = L.cont_group;
+    while (g < 64 && (long long)g * 4096 < (long long)n) g *= 2;
+    return g;
+}
+
 __device__ __forceinline__ int n_items(const RtLaunch &L)
 {
     if (L.level == 0) return ((L.cam.width + 7) >> 3) * ((L.rows + 7) >> 3);
-    const int g = L.cont_group;
+    const int g = cont_g(L);
     return (*lvl_ctr(L, L.level - 1) + g - 1) / g;
 }
 
@@ -1056,8 +1068,9 @@ __device__ __forceinline__ void ray_src(const RtLaunch &L, int item, int lane, R
         const size_t di = (size_t)x * (size_t)L.rows + (size_t)lr;           // x-major (k_frame_start)
         for (int i = 0; i < 3; i++) { r.o[i] = L.cam.pos[i]; r.d[i] = L.dirs[(size_t)i * plane + di]; }
     } else {
-        const int q = item * L.cont_group + lane;
-        r.valid = lane < L.cont_group && q < *lvl_ctr(L, L.level - 1);
+        const int g = cont_g(L);
+        const int q = item * g + lane;
+        r.valid = lane < g && q < *lvl_ctr(L, L.level - 1);
         if (!r.valid) return;
         r.id = (size_t)q;
         r.rec = L.queue[(L.level - 1) & 1] + q;

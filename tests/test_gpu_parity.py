@@ -306,6 +306,25 @@ def test_split_equals_fused(ctx, name, monkeypatch):
             c.close()
 
 
+@pytest.mark.parametrize("group", ["1", "16", "64"])
+def test_continuation_rays_per_wave(ctx, group, monkeypatch):
+    """Bounce levels take RT_CONT_GROUP rays per wave, up to 64 when a level is large (cont_g:
+    config 5's millions of bounce rays); the width changes scheduling, not results.  Unsegmented
+    levels (RT_SEG=0), refmax 5, mirrors and transmission: identical to the oracle."""
+    spec = _transmission_spec()
+    cam, cfg = scenes.make_camera(160, 120), scenes.make_config(5)
+    monkeypatch.setenv("RT_SEG", "0")
+    monkeypatch.setenv("RT_CONT_GROUP", group)
+    c = rtamd.Context(0)
+    try:
+        c.upload(rtamd.build_scene(spec))
+        got = c.trace_frame(cam, cfg, stats=False, allow_fault=True)
+    finally:
+        c.close()
+    w, root = oracle.build_scene(spec)
+    _compare(w.trace_frame(root, cam, cfg, nthreads=8), got)
+
+
 def _transmission_spec():
     spec = scenes.small_random(5)
     sh = spec.shades.copy()
