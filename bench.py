@@ -336,7 +336,7 @@ def main():
 
     if rank == 0:
         rec = {
-            "metric": "Mrays/s (whole node) at 1920x1080",
+            "metric": "Mrays/s (whole node) at %dx%d" % (W, H),
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
