@@ -1,25 +1,39 @@
 """bench.py — Mrays/s and ms/frame of the MI355X render path (BASELINE.json metric).
 
-A step is one frame: ray generation + trace + (N>1) RCCL gather of the row stripes to rank 0 and
-de-interleave into the 1920x1080 frame.  The frame is split across ranks (strong scaling: the
+A step is one frame: ray generation + trace + (N>1) the gather of the row stripes on the first GPU
+and their de-interleave into the W x H frame.  The frame is split across GPUs (strong scaling: the
 frame size is fixed).  Inputs (scene, camera) are resident on the GPU before the timed region.
 
-Frames in flight (--inflight P, default 16): each rank keeps P contexts, each on its own HIP
-stream with its own frame buffers, and issues frame f on context f % P.  HIP maps streams onto
-GPU_MAX_HW_QUEUES hardware queues (HIP's default is 4); the bench raises it to 16 before the HIP
-runtime starts, so that 16 frames really run concurrently.  A frame's bounce level 1
-is a latency-bound tail (few, long continuation rays) that the next frames' primary
-passes fill.  Every one of the K timed frames is rendered and gathered completely inside the timed
-region; `value` is their throughput.  A serial pass (one frame in flight) reports the per-frame
-latency beside it (`serial`) and is what the roofline's kernel duration is measured on.
+How N GPUs run:
+  * under torchrun (WORLD_SIZE set; the driver's N>1 launch): one process per GPU, each rendering
+    its stripes with rt_trace_rows_device; one torch.distributed gather (RCCL over xGMI) brings the
+    stripes to rank 0.  WORLD_SIZE must equal --gpus.
+  * `python bench.py --gpus N` without torchrun: one process, one librt context over N GPUs (the
+    product path behind rt_create / the JS drop-in's options.devices): the context splits the
+    frame, traces every part on its GPU and gathers on GPU 0 with RCCL inside librt.  Fails (exit 2)
+    when fewer than N GPUs exist.
+
+Frames in flight (--inflight P, default 16; 4 for the one-process multi-GPU mode): P contexts, each
+on its own HIP stream with its own frame buffers; frame f runs on context f % P.  HIP maps streams
+onto GPU_MAX_HW_QUEUES hardware queues (HIP's default is 4); the bench raises it to 16 before the
+HIP runtime starts.  A frame's bounce level is a latency-bound tail (few, long continuation rays;
+DESIGN.md §6.2) that the next frames' primary passes fill.  Every timed frame is rendered and
+gathered completely inside the timed region; `value` is their throughput.  A serial pass (one frame
+in flight) reports the per-frame latency beside it (`serial`).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config config3]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0 (schema in the task contract) including `roofline` for the trace
-kernel (algorithmic bytes per launch from the kernel's own work counters, SURVEY.md §8d, over the
-HIP-event-timed kernel duration) and `cpu_baseline` (the oracle restatement, single-threaded, on a
-bounded pixel sample of the same workload).
+Prints ONE JSON line on rank 0.  Beside `value` it reports:
+  roofline      per trace kernel (k_walk, k_first, k_shade, ...) from rocprofv3 (kernel-trace and
+                four --pmc passes, N=1): duration, VALU-issue fraction and lane utilisation (the
+                binding roof of this branchy binary64 traversal), HBM traffic (2*FETCH_SIZE +
+                WRITE_SIZE) as a fraction of 8 TB/s, and the §8(d) algorithmic bytes (cache-served,
+                labelled so); the headline entry is the dominant kernel against the roof that binds.
+  host_frame    rt_trace_frame (host Float32Array in and out, what the JS drop-in calls): median
+                wall time of 10 frames after 3 warm-ups (SURVEY §8(d) ms/frame), PCIe included.
+  cpu_baseline  the oracle restatement (plain C) on a bounded pixel sample, 1 thread and all the
+                cores this process may use, with the host CPU model.
 """
 import os
 
@@ -32,6 +46,8 @@ import argparse
 import csv
 import glob
 import json
+import math
+import re
 import shutil
 import subprocess
 import sys
@@ -51,21 +67,66 @@ from rtamd import abi  # noqa: E402
 from rtamd.stripes import StripeGather  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-# Algorithmic bytes per unit of work of the reference's algorithm (canonical f64
-# layout) over the reference-equivalent counters: what the in-order entity scan would read.
-BYTES_REF = dict(n_ret=48, n_slot=32, n_loc=40, n_sph=36, n_box=36, n_tri=76, n_hit=40, primary=12)
-# Algorithmic bytes of the work k_trace actually performs: walker records as above,
-# 32 B per cull-hierarchy box test, 80 B per exact entity test (record + rank), 44 B per hit (shade
-# record + entity id), 36 B per pixel (24 B direction read + 12 B RGB store).
+SIMDS = 256 * 4                # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4                # peak engine clock
+# VALU issue cost in cycles per wave64 instruction on one SIMD (MI355X_MICROARCH.md: a wave issues
+# a VALU instruction over 2 cycles; binary64 runs at half the f32 rate, 78.6 vs 157.3 TF/s; f64
+# transcendentals (v_rcp/v_sqrt/v_rsq_f64) taken at a quarter of that, an assumption)
+ISSUE_CYC, ISSUE_CYC_F64, ISSUE_CYC_F64_TRANS = 2, 4, 16
+# §8(d) algorithmic bytes of the work each pass performs: walker records (48 B per
+# returned node, 32 B per slot step, 40 B per point-location level), 32 B per cull-hierarchy box
+# test, 80 B per exact entity test, 44 B per hit (shade + entity id), 36 B per segment (direction
+# or record in, RGB out).  Served from L2 / Infinity Cache for the most part: "cache-served".
+PASS_BYTES = {"walk": dict(n_ret=48, n_slot=32, n_loc=40), "first": dict(n_cull=32, n_exact=80),
+              "shade": dict(n_hit=44, segments=36)}
 BYTES_KERNEL = dict(n_ret=48, n_slot=32, n_loc=40, n_cull=32, n_exact=80, n_hit=44, primary=36)
+BYTES_REF = dict(n_ret=48, n_slot=32, n_loc=40, n_sph=36, n_box=36, n_tri=76, n_hit=40, primary=12)
+KERNEL_PASS = {"k_walk": "walk", "k_walk_seg": "walk", "k_first": "first", "k_first_seg": "first",
+               "k_shade": "shade"}
+TRACE_KERNELS = ("k_walk", "k_walk_seg", "k_first", "k_first_seg", "k_shade", "k_cont", "k_trace", "k_frame_start")
+PMC_FRAMES = 4                 # frames the --pmc-child run traces
+PMC_PASSES = {
+    "fetch": ["FETCH_SIZE"],
+    "write": ["WRITE_SIZE"],
+    "valu": ["SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+             "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_INSTS_BRANCH"],
+    "lanes": ["SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+              "GRBM_GUI_ACTIVE"],
+}
 
 
 def algorithmic_bytes(counters, table):
     return sum(table[k] * counters[k] for k in table)
 
 
+# ---- CPU baseline ------------------------------------------------------------------------------------
+def usable_cores():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota when one is set
+    (the GPU box shows the whole machine's CPUs but grants a share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(math.ceil(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(spec, cam, cfg, budget_s):
-    """Oracle restatement (plain C, 1 thread) on a random pixel sample; Mrays/s of traced segments."""
+    """Oracle restatement (plain C) on a random pixel sample: 1 thread for ~budget_s, then the same
+    sample on every usable core.  Mrays/s of traced segments."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     w, root = oracle.build_scene(spec)
@@ -81,69 +142,142 @@ def cpu_baseline(spec, cam, cfg, budget_s):
         segs += r["counters"]["segments"]
         done += len(pix)
         chunk = min(chunk * 2, 65536) if t_used < budget_s / 4 else chunk
-    # the same sample split over the host's CPU share (a worker split across all cores)
-    nt = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    nt, visible, quota = usable_cores()
     t0 = time.perf_counter()
     r = w.trace_frame(root, cam, cfg, pixels=order[:done], nthreads=nt)
     t_mt = time.perf_counter() - t0
     w.close()
+    model = cpu_model()
     return dict(value=segs / t_used / 1e6, unit="Mrays/s", cores=1, kind="port",
                 sample="%d random pixels of the %dx%d frame (%d segments) in %.1f s, oracle/rt_oracle.c, 1 thread"
                        % (done, cam.width, cam.height, segs, t_used),
+                cpu_model=model, cpus_visible=visible, cpu_quota=quota,
                 threaded=dict(value=r["counters"]["segments"] / t_mt / 1e6, unit="Mrays/s", cores=nt,
-                              sample="the same pixels, %d threads, %.2f s" % (nt, t_mt)))
+                              sample="the same pixels on %d threads (all usable cores), %.2f s" % (nt, t_mt)))
 
 
-TRACE_KERNELS = ("k_walk", "k_first", "k_shade", "k_cont", "k_trace")
-PMC_FRAMES = 4                 # frames the --pmc-child run traces (warmup 1 + steps 3)
+# ---- rocprofv3 passes (N = 1) ------------------------------------------------------------------------
+def _kernel_base(name):
+    m = re.search(r"(k_[a-z_]+?)(?:<|\(|$)", name.split("::")[-1])
+    return m.group(1) if m else None
 
 
-def _pmc_pass(counter, config, stripe, timeout_s):
-    """One rocprofv3 --pmc pass over a child bench run; counter total per frame over the trace
-    kernels (the stats instantiation k_trace<true, ...> is not part of a frame)."""
+def _child_cmd(args):
+    return [sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
+            "--stripe", str(args.stripe)]
+
+
+def _rocprof(extra, args, timeout_s, keep=None):
+    """One rocprofv3 run over the --pmc-child frame loop; returns (out_dir, error)."""
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None, "rocprofv3 not on PATH"
-    out = tempfile.mkdtemp(prefix="rt_pmc_")
+    out = tempfile.mkdtemp(prefix="rt_prof_")
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    cmd = [prof] + extra + ["-d", out, "-o", "p", "--output-format", "csv", "--"] + _child_cmd(args)
     try:
-        env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [prof, "--pmc", counter, "-d", out, "-o", "pmc", "--output-format", "csv", "--",
-               sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", config,
-               "--stripe", str(stripe), "--steps", "3", "--warmup", "1"]
         r = subprocess.run(cmd, env=env, timeout=timeout_s, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
-        if r.returncode != 0:
-            tail = r.stdout.decode(errors="replace").strip().splitlines()[-3:]
-            return None, "%s pass exit %d: %s" % (counter, r.returncode, " | ".join(tail))
-        vals = []
-        for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+    except subprocess.TimeoutExpired:
+        shutil.rmtree(out, ignore_errors=True)
+        return None, "%s: timed out" % " ".join(extra[:2])
+    if r.returncode != 0:
+        tail = r.stdout.decode(errors="replace").strip().splitlines()[-3:]
+        shutil.rmtree(out, ignore_errors=True)
+        return None, "%s: exit %d: %s" % (" ".join(extra[:2]), r.returncode, " | ".join(tail))
+    return out, None
+
+
+def kernel_durations(args, timeout_s=300):
+    """Per-kernel time per frame (ms) from rocprofv3 --kernel-trace --stats over PMC_FRAMES frames;
+    the stats CSV is kept under --profile-out."""
+    out, err = _rocprof(["--kernel-trace", "--stats"], args, timeout_s)
+    if err:
+        return None, err
+    try:
+        dur = {}
+        for f in glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    name = r["Kernel_Name"]
-                    stats = "<true" in name or "ILb1E" in name
-                    if any(k in name for k in TRACE_KERNELS) and not stats and r["Counter_Name"] == counter:
-                        vals.append(float(r["Counter_Value"]))
-        if not vals:
-            return None, "%s pass: no trace-kernel rows in the counter CSV" % counter
-        return sum(vals) / PMC_FRAMES, None
-    except Exception as e:  # the bench line must not depend on the profiler
-        return None, "%s pass: %r" % (counter, e)
+                    k = _kernel_base(r["Kernel_Name"])
+                    if k in TRACE_KERNELS:
+                        dur[k] = dur.get(k, 0.0) + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+        if args.profile_out:
+            os.makedirs(args.profile_out, exist_ok=True)
+            for f in glob.glob(os.path.join(out, "**", "*kernel_stats.csv"), recursive=True):
+                shutil.copy(f, os.path.join(args.profile_out, "kernel_stats_%s.csv" % args.config))
+        if not dur:
+            return None, "kernel trace: no trace-kernel rows"
+        return {k: v / PMC_FRAMES for k, v in dur.items()}, None
     finally:
         shutil.rmtree(out, ignore_errors=True)
 
 
-def hbm_traffic(config, stripe, timeout_s=300):
-    """HBM bytes per frame's trace kernels from PMC (MI355X_MICROARCH.md HBM section): FETCH_SIZE
-    and WRITE_SIZE in separate passes (TCC slots), both in KiB; FETCH_SIZE doubled (gfx950 tallies
-    128-B requests at 64 B).  None when rocprofv3 or a pass is unavailable."""
-    fetch, err = _pmc_pass("FETCH_SIZE", config, stripe, timeout_s)
-    if err:
-        return None, err
-    write, err = _pmc_pass("WRITE_SIZE", config, stripe, timeout_s)
-    if err:
-        return None, err
-    return dict(bytes=2 * fetch * 1024 + write * 1024, fetch_kib_raw=fetch, write_kib=write,
-                method="rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes), summed over one frame's trace "
-                       "kernels: 2*FETCH_SIZE + WRITE_SIZE"), None
+def pmc_counters(args, timeout_s=300):
+    """Counter totals per frame and trace kernel over the PMC_PASSES (one rocprofv3 --pmc run each:
+    counter slots per block are limited; MI355X_MICROARCH.md)."""
+    tot, notes = {}, []
+    for name, counters in PMC_PASSES.items():
+        out, err = _rocprof(["--pmc"] + counters, args, timeout_s)
+        if err:
+            notes.append(err)
+            continue
+        try:
+            for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for r in csv.DictReader(fh):
+                        k = _kernel_base(r["Kernel_Name"])
+                        if k in TRACE_KERNELS and r["Counter_Name"] in counters:
+                            d = tot.setdefault(k, {})
+                            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"]) / PMC_FRAMES
+        finally:
+            shutil.rmtree(out, ignore_errors=True)
+    if args.profile_out and tot:
+        os.makedirs(args.profile_out, exist_ok=True)
+        with open(os.path.join(args.profile_out, "pmc_%s.json" % args.config), "w") as fh:
+            json.dump(dict(per_frame=tot, frames=PMC_FRAMES, passes=PMC_PASSES), fh, indent=1, sort_keys=True)
+    return tot, notes
+
+
+def kernel_rooflines(dur, pmc, counters):
+    """Per trace kernel: which roof binds.  VALU issue: issue cycles (f64 weighted)
+    over SIMDs x the kernel's measured clock (GRBM_GUI_ACTIVE / 8 per XCD) x its duration; lanes:
+    SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU of 64; HBM: 2*FETCH_SIZE + WRITE_SIZE (KiB; FETCH_SIZE
+    doubled on gfx950) over the duration against 8 TB/s; algorithmic bytes (§8(d), cache-served)."""
+    out = {}
+    for k, ms in sorted(dur.items(), key=lambda kv: -kv[1]):
+        c = pmc.get(k, {})
+        e = dict(ms_per_frame=round(ms, 4))
+        s = ms * 1e-3
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            b = 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
+            e.update(hbm_bytes=int(b), hbm_GBps=round(b / s / 1e9, 1), hbm_frac=round(b / s / 1e9 / HBM_PEAK_GBS, 4))
+        if "SQ_INSTS_VALU" in c:
+            f64 = sum(c.get(x, 0.0) for x in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"))
+            tr = c.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+            cyc = ISSUE_CYC * (c["SQ_INSTS_VALU"] - f64 - tr) + ISSUE_CYC_F64 * f64 + ISSUE_CYC_F64_TRANS * tr
+            e.update(valu_insts=int(c["SQ_INSTS_VALU"]), f64_insts=int(f64 + tr), salu_insts=int(c.get("SQ_INSTS_SALU", 0)),
+                     branch_insts=int(c.get("SQ_INSTS_BRANCH", 0)), valu_issue_cycles=int(cyc),
+                     valu_issue_frac_peak_clock=round(cyc / (SIMDS * CLOCK_GHZ * 1e9 * s), 4))
+            if c.get("GRBM_GUI_ACTIVE"):
+                clk = c["GRBM_GUI_ACTIVE"] / 8 / s
+                e.update(clock_ghz=round(clk / 1e9, 3), valu_issue_frac=round(cyc / (SIMDS * clk * s), 4))
+        if c.get("SQ_ACTIVE_INST_VALU"):
+            lanes = c["SQ_THREAD_CYCLES_VALU"] / c["SQ_ACTIVE_INST_VALU"]
+            e.update(active_lanes=round(lanes, 2), lane_util=round(lanes / 64, 4))
+        if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in c:
+            e.update(wait_frac=round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4))
+        p = KERNEL_PASS.get(k)
+        if p:
+            # the pass's algorithmic bytes are shared by its kernels in proportion to their time
+            share = ms / sum(v for kk, v in dur.items() if KERNEL_PASS.get(kk) == p)
+            ab = algorithmic_bytes(counters, PASS_BYTES[p]) * share
+            e.update(alg_bytes_cache_served=int(ab), alg_GBps=round(ab / s / 1e9, 1),
+                     alg_frac_of_hbm_peak=round(ab / s / 1e9 / HBM_PEAK_GBS, 4))
+        roofs = {r: e[f] for r, f in (("valu-issue", "valu_issue_frac"), ("hbm", "hbm_frac")) if f in e}
+        if roofs:
+            e["binding_roof"] = max(roofs, key=roofs.get)
+        out[k] = e
+    return out
 
 
 def exposure_bench(ctx, frame, stream, reps=20):
@@ -174,38 +308,45 @@ def exposure_bench(ctx, frame, stream, reps=20):
                 mean=st.mean, variance=st.variance, range=[lo, hi])
 
 
+def host_frame_time(ctx, cam, cfg, segments, warm=3, reps=10):
+    """SURVEY §8(d) ms/frame: rt_trace_frame with a host Float32Array (camera in, kernels, gather,
+    D2H into the ebuffer) — what the JS drop-in's trace_frame() costs.  Median of `reps` after `warm`."""
+    rgb = np.zeros(cam.width * cam.height * 3, np.float32)
+    for _ in range(warm):
+        ctx.trace_frame(cam, cfg, rgb=rgb, ids=False, stats=False)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.trace_frame(cam, cfg, rgb=rgb, ids=False, stats=False)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    med = float(np.median(ts))
+    return dict(entry="rt_trace_frame (host RGB buffer, D2H included)", warmup=warm, frames=reps,
+                ms_per_frame_median=round(med, 3), ms_min=round(min(ts), 3), ms_max=round(max(ts), 3),
+                value=round(segments / (med * 1e-3) / 1e6, 3), unit="Mrays/s")
+
+
 def pmc_child(args):
-    """Minimal frame loop profiled by hbm_traffic(): no stats launch, no CPU baseline, no output."""
+    """Minimal frame loop profiled by the rocprofv3 passes: no stats launch, no CPU baseline, no output."""
     factory, W, H, refmax = scenes.WORKLOADS[args.config]
     ctx = rtamd.Context(0)
     ctx.upload(rtamd.build_scene(factory()))
     cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
     buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
     s = torch.cuda.Stream()
+    torch.cuda.synchronize()
     for _ in range(PMC_FRAMES):
         ctx.trace_rows_device(cam, cfg, 0, 1, args.stripe, buf.data_ptr(), s.cuda_stream)
     s.synchronize()
     ctx.close()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="config3", choices=sorted(scenes.WORKLOADS))
-    ap.add_argument("--stripe", type=int, default=8, help="rows per stripe of the row-interleaved split")
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
-    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
-    ap.add_argument("--inflight", type=int, default=16, help="frames in flight per rank (contexts / streams)")
-    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    args = ap.parse_args()
-    if args.pmc_child:
-        return pmc_child(args)
+def fail(msg):
+    print("bench.py: " + msg, file=sys.stderr, flush=True)
+    sys.exit(2)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+# ---- one process per GPU (torchrun) or a single GPU -----------------------------------------------------
+def run_ranks(args, spec, scene, W, H, refmax, world, rank, local):
     if os.environ.get("RT_BENCH_BACKEND") == "gloo":
         local %= torch.cuda.device_count()       # plumbing check: ranks may share the box's one GPU
     torch.cuda.set_device(local)
@@ -213,13 +354,9 @@ def main():
     if world > 1:
         backend = os.environ.get("RT_BENCH_BACKEND", "nccl")   # "gloo": plumbing checks with ranks sharing a GPU
         dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
-
-    factory, W, H, refmax = scenes.WORKLOADS[args.config]
-    spec = factory()
-    t0 = time.perf_counter()
-    scene = rtamd.build_scene(spec)
-    build_s = time.perf_counter() - t0
-    P = max(1, min(args.inflight, args.steps))
+        if dist.get_world_size() != args.gpus:
+            fail("torch.distributed world size %d != --gpus %d" % (dist.get_world_size(), args.gpus))
+    P = max(1, min(args.inflight or 16, args.steps))
     ctxs = []
     for _ in range(P):
         c = rtamd.Context(local)
@@ -235,7 +372,6 @@ def main():
     sp = stream.cuda_stream
     sgs = [StripeGather(H, W, rank, world, args.stripe, dev) for _ in range(P)]
     sg = sgs[0]
-    local_buf = sg.local
 
     def step(f, inflight):
         i = f % inflight
@@ -244,21 +380,14 @@ def main():
                                       streams[i].cuda_stream)
             sgs[i].gather()        # the collective waits for this stream; this stream for it
 
-    def timed(inflight, steps, warmup):
-        for f in range(warmup):
-            step(f, inflight)
+    def sync():
         torch.cuda.synchronize(dev)
+
+    def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for f in range(steps):
-            step(f, inflight)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        el = time.perf_counter() - t0
+
+    def max_over_ranks(el):
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -266,105 +395,219 @@ def main():
         return el
 
     # work counters of one frame (untimed STATS launch): segments and algorithmic bytes
-    _, st = ctx.trace_rows_device(cam, cfg, rank, world, args.stripe, local_buf.data_ptr(), sp, stats=True)
+    _, st = ctx.trace_rows_device(cam, cfg, rank, world, args.stripe, sg.local.data_ptr(), sp, stats=True)
     counters = dict(st.counters(), **st.work())
     names = st.COUNTERS + st.WORK
     ctr = torch.tensor([counters[k] for k in names], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(ctr)
     tot = dict(zip(names, ctr.tolist()))
-    local_bytes = algorithmic_bytes(counters, BYTES_KERNEL)
-    local_bytes_ref = algorithmic_bytes(counters, BYTES_REF)
 
-    elapsed = timed(P, args.steps, max(args.warmup, P))
+    res = timed_runs(args, P, step, sync, barrier, max_over_ranks)
     # every in-flight slot rendered the same camera: their gathered frames must agree bit for bit
     same = all(torch.equal(sgs[i].frame.view(torch.int32), sgs[0].frame.view(torch.int32)) for i in range(1, P)) \
         if rank == 0 else None
     # N > 1: rank 0's gathered frame equals the whole frame rendered on its own GPU alone
     if world > 1 and rank == 0:
         whole = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
-        torch.cuda.synchronize(dev)
+        sync()
         ctx.trace_rows_device(cam, cfg, 0, 1, H, whole.data_ptr(), sp)
-        torch.cuda.synchronize(dev)
+        sync()
         same = bool(same) and torch.equal(whole.view(torch.int32), sgs[0].frame.view(torch.int32))
-    # serial pass: one frame in flight on context 0; its HIP events give the kernel duration
-    elapsed_serial = timed(1, args.steps, 1) if P > 1 else elapsed
     kt = ctx.kernel_times(args.steps)
-    k_ms = float(np.mean(kt)) if len(kt) else float("nan")
-
-    ms_per_step = elapsed / args.steps * 1e3
-    value = tot["segments"] * args.steps / elapsed / 1e6
-    serial = dict(frames_in_flight=1, ms_per_frame=round(elapsed_serial / args.steps * 1e3, 4),
-                  value=round(tot["segments"] * args.steps / elapsed_serial / 1e6, 3), unit="Mrays/s")
-    achieved = local_bytes / (k_ms * 1e-3) / 1e9 if k_ms == k_ms and k_ms > 0 else None
-    roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=(achieved / HBM_PEAK_GBS) if achieved else None, traffic=None,
-                    kernel="trace (k_walk + k_first + k_shade per bounce level, k_cont)", kernel_ms=k_ms,
-                    bytes_per_launch=local_bytes,
-                    bytes_formula="48*n_ret+32*n_slot+40*n_loc+32*n_cull+80*n_exact+44*n_hit+36*primary",
-                    bytes_reference_equivalent=local_bytes_ref,
-                    reference_equivalent_formula="SURVEY 8d: 48*n_ret+32*n_slot+40*n_loc+36*n_sph+36*n_box+76*n_tri+40*n_hit+12*primary")
-
-    # PCIe-inclusive rate of the host-buffer entry point (rt_trace_frame: RGB copied back to a host
-    # Float32Array-sized buffer each frame) — reported beside `value`, never as it
-    host = None
-    if rank == 0 and world == 1:
-        rgb_host = np.zeros(W * H * 3, np.float32)
-        ctx.trace_frame(cam, cfg, rgb=rgb_host, ids=False, stats=False)
-        t0 = time.perf_counter()
-        n_host = 3
-        for _ in range(n_host):
-            ctx.trace_frame(cam, cfg, rgb=rgb_host, ids=False, stats=False)
-        host_ms = (time.perf_counter() - t0) / n_host * 1e3
-        host = dict(entry="rt_trace_frame (host RGB buffer)", ms_per_frame=round(host_ms, 3),
-                    value=round(tot["segments"] / (host_ms * 1e-3) / 1e6, 3), unit="Mrays/s")
-
-    exposure = exposure_bench(ctx, sg.frame, stream) if rank == 0 else None
-
-    traffic = None
-    if rank == 0 and world == 1 and not args.no_traffic:
-        traffic, err = hbm_traffic(args.config, args.stripe)
-        if traffic is not None:
-            roofline["traffic"] = traffic["bytes"]
-            roofline["traffic_detail"] = traffic
-        else:
-            roofline["traffic_note"] = err
-
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
-        cpu = cpu_baseline(spec, cam, cfg, args.cpu_budget)
-
-    if rank == 0:
-        rec = {
-            "metric": "Mrays/s (whole node) at %dx%d" % (W, H),
-            "value": round(value, 3),
-            "unit": "Mrays/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (splitmix64 seed 42 scene, BASELINE.json %s)" % args.config,
-            "config": {"workload": args.config, "scene": spec.name, "width": W, "height": H, "refmax": refmax,
-                       "entities": int(len(spec.entities)), "octree_nodes": int(scene.n_nodes),
-                       "segments_per_frame": tot["segments"], "parallelism": "rows%d/stripe%d" % (world, args.stripe),
-                       "frames_in_flight": P, "frames_identical": same,
-                       "counters": tot, "scene_build_s": round(build_s, 3)},
-            "roofline": roofline,
-            "serial": serial,
-            "cpu_baseline": cpu,
-            "pcie_inclusive": host,
-            "exposure": exposure,
-            "mpixels_per_s": round(W * H * args.steps / elapsed / 1e6, 3),
-        }
-        print(json.dumps(rec), flush=True)
+    extra = dict(mode="one process per GPU" if world > 1 else "one GPU", collective="torch.distributed.gather (RCCL)"
+                 if world > 1 else None, n_gpus=dist.get_world_size() if world > 1 else 1)
+    host = host_frame_time(ctx, cam, cfg, tot["segments"]) if rank == 0 and world == 1 else None
+    expo = exposure_bench(ctx, sg.frame, stream) if rank == 0 else None
+    out = dict(res, tot=tot, counters=counters, same=same, kernel_ms=float(np.mean(kt)) if len(kt) else None,
+               host=host, exposure=expo, P=P, **extra)
     for c in ctxs:
         c.close()
     if world > 1:
         dist.destroy_process_group()
+    return out, rank
+
+
+# ---- one process, one librt context over N GPUs (the product's multi-GPU path) ---------------------------
+def run_devices(args, spec, scene, W, H, refmax, n):
+    devs = list(range(n))
+    P = max(1, min(args.inflight or 4, args.steps))
+    ctxs = []
+    for _ in range(P):
+        c = rtamd.Context(devices=devs, stripe_rows=args.stripe)
+        c.upload(scene)
+        ctxs.append(c)
+    ctx = ctxs[0]
+    info = ctx.info()
+    if info["n_devices"] != n:
+        fail("context spans %d devices, --gpus %d" % (info["n_devices"], n))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(P)]
+    frames = [torch.zeros((H, W, 3), dtype=torch.float32, device=dev) for _ in range(P)]
+    torch.cuda.synchronize(dev)
+
+    def step(f, inflight):
+        i = f % inflight
+        ctxs[i].trace_frame_device(cam, cfg, frames[i].data_ptr(), streams[i].cuda_stream)
+
+    def sync():
+        for d in devs:
+            torch.cuda.synchronize(d)
+
+    r = ctx.trace_frame(cam, cfg, ids=False, stats=True)      # counters summed over the devices
+    counters = dict(r["stats"].counters(), **r["stats"].work())
+    tot = dict(counters)
+    res = timed_runs(args, P, step, sync, lambda: None, lambda el: el)
+    same = all(torch.equal(frames[i].view(torch.int32), frames[0].view(torch.int32)) for i in range(1, P))
+    one = rtamd.Context(0)
+    one.upload(scene)
+    whole = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
+    one.trace_frame_device(cam, cfg, whole.data_ptr(), streams[0].cuda_stream)
+    sync()
+    same = bool(same) and torch.equal(whole.view(torch.int32), frames[0].view(torch.int32))
+    one.close()
+    host = host_frame_time(ctx, cam, cfg, tot["segments"])
+    out = dict(res, tot=tot, counters=counters, same=same, kernel_ms=None, host=host, exposure=None, P=P,
+               mode="one process, one librt context over %d GPUs" % n,
+               collective="ncclGather inside librt (%s)" % info["gather"], n_gpus=n)
+    for c in ctxs:
+        c.close()
+    return out, 0
+
+
+def timed_runs(args, P, step, sync, barrier, max_over_ranks):
+    def timed(inflight, steps, warmup):
+        for f in range(warmup):
+            step(f, inflight)
+        sync()
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        for f in range(steps):
+            step(f, inflight)
+        sync()
+        barrier()
+        sync()
+        return max_over_ranks(time.perf_counter() - t0)
+
+    warm = max(args.warmup, P)     # every in-flight slot renders once before timing
+    el = timed(P, args.steps, warm)
+    el_serial = timed(1, args.steps, 1) if P > 1 else el
+    return dict(elapsed=el, elapsed_serial=el_serial, warmup_frames=warm)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="config3", choices=sorted(scenes.WORKLOADS))
+    ap.add_argument("--stripe", type=int, default=8, help="rows per stripe of the row-interleaved split")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
+    ap.add_argument("--no-traffic", "--no-profile", dest="no_profile", action="store_true",
+                    help="skip the rocprofv3 kernel-trace / PMC passes")
+    ap.add_argument("--profile-out", default=None, help="keep the rocprofv3 summaries (kernel stats, PMC) here")
+    ap.add_argument("--inflight", type=int, default=0, help="frames in flight (contexts / streams); 0 = default")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.pmc_child:
+        return pmc_child(args)
+    if args.gpus < 1:
+        fail("--gpus must be >= 1")
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != args.gpus:
+        fail("WORLD_SIZE=%s but --gpus %d: launch one rank per GPU (torchrun --nproc-per-node %d)"
+             % (env_world, args.gpus, args.gpus))
+    single_process_multi = env_world is None and args.gpus > 1
+    have = torch.cuda.device_count()              # counts devices without initialising HIP here
+    if env_world is None and have < args.gpus:
+        fail("--gpus %d needs %d GPUs, this host has %d" % (args.gpus, args.gpus, have))
+    if env_world is not None and os.environ.get("RT_BENCH_BACKEND") != "gloo" and \
+            int(os.environ.get("LOCAL_RANK", "0")) >= have:
+        fail("LOCAL_RANK %s has no GPU (this host has %d)" % (os.environ.get("LOCAL_RANK"), have))
+
+    factory, W, H, refmax = scenes.WORKLOADS[args.config]
+    spec = factory()
+    t0 = time.perf_counter()
+    scene = rtamd.build_scene(spec)
+    build_s = time.perf_counter() - t0
+
+    if single_process_multi:
+        res, rank = run_devices(args, spec, scene, W, H, refmax, args.gpus)
+    else:
+        world = int(env_world or 1)
+        res, rank = run_ranks(args, spec, scene, W, H, refmax, world, int(os.environ.get("RANK", "0")),
+                              int(os.environ.get("LOCAL_RANK", "0")))
+    if rank != 0:
+        return
+    tot, el, steps = res["tot"], res["elapsed"], args.steps
+    n_gpus = res["n_gpus"]
+    value = tot["segments"] * steps / el / 1e6
+    serial = dict(frames_in_flight=1, ms_per_frame=round(res["elapsed_serial"] / steps * 1e3, 4),
+                  value=round(tot["segments"] * steps / res["elapsed_serial"] / 1e6, 3), unit="Mrays/s")
+
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
+    roofline = dict(bound=None, achieved=None, peak=None, unit=None, frac=None, traffic=None,
+                    trace_kernels_ms_hip_events=res["kernel_ms"],
+                    algorithmic_bytes_per_frame=algorithmic_bytes(tot, BYTES_KERNEL),
+                    reference_equivalent_bytes_per_frame=algorithmic_bytes(tot, BYTES_REF))
+    if n_gpus == 1 and not args.no_profile:
+        dur, err = kernel_durations(args)
+        pmc, notes = pmc_counters(args) if dur else ({}, [])
+        if dur:
+            kr = kernel_rooflines(dur, pmc, tot)
+            roofline["kernels"] = kr
+            roofline["kernel_ms_rocprof_sum"] = round(sum(dur.values()), 4)
+            top = max(kr, key=lambda k: kr[k]["ms_per_frame"])
+            t = kr[top]
+            if "valu_issue_frac" in t or "hbm_frac" in t:
+                bound = t.get("binding_roof", "valu-issue")
+                if bound == "valu-issue":
+                    slots = t["valu_issue_cycles"] / ISSUE_CYC
+                    roofline.update(bound="valu-issue", achieved=round(slots / (t["ms_per_frame"] * 1e-3) / 1e9, 2),
+                                    peak=round(SIMDS * t["clock_ghz"] / ISSUE_CYC, 1), unit="G VALU issue slots/s",
+                                    frac=t["valu_issue_frac"])
+                else:
+                    roofline.update(bound="hbm", achieved=t["hbm_GBps"], peak=HBM_PEAK_GBS, unit="GB/s",
+                                    frac=t["hbm_frac"])
+                roofline.update(kernel=top, traffic=t.get("hbm_bytes"), lane_util=t.get("lane_util"),
+                                note="dominant kernel against the roof that binds it: VALU issue (f64 at 4 "
+                                     "cycles, others at 2 per wave64 instruction per SIMD, at the kernel's "
+                                     "measured clock); HBM traffic = 2*FETCH_SIZE + WRITE_SIZE per frame")
+        if err or notes:
+            roofline["profile_notes"] = [x for x in [err] + notes if x]
+
+    cpu = cpu_baseline(spec, cam, cfg, args.cpu_budget) if args.cpu_budget > 0 and n_gpus == 1 else None
+    rec = {
+        "metric": "Mrays/s (whole node) at %dx%d" % (W, H),
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": n_gpus,
+        "steps": steps,
+        "warmup": res["warmup_frames"],
+        "ms_per_step": round(el / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (splitmix64 seed 42 scene, BASELINE.json %s)" % args.config,
+        "config": {"workload": args.config, "scene": spec.name, "width": W, "height": H, "refmax": refmax,
+                   "entities": int(len(spec.entities)), "octree_nodes": int(scene.n_nodes),
+                   "segments_per_frame": tot["segments"],
+                   "parallelism": "rows%d/stripe%d" % (n_gpus, args.stripe), "mode": res["mode"],
+                   "collective": res["collective"], "frames_in_flight": res["P"],
+                   "frames_identical": res["same"], "counters": tot, "scene_build_s": round(build_s, 3)},
+        "roofline": roofline,
+        "serial": serial,
+        "host_frame": res["host"],
+        "cpu_baseline": cpu,
+        "exposure": res["exposure"],
+        "mpixels_per_s": round(W * H * steps / el / 1e6, 3),
+    }
+    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

@@ -19,7 +19,9 @@
  *
  * Plain C types only (no torch / HIP types).  All functions return RT_OK (0) or a negative RT_E_*
  * code and set a thread-local message readable with rt_last_error().  No C++ exception crosses
- * the ABI.  A context is bound to one GPU and is not re-entrant.
+ * the ABI.  A context drives 1..RT_MAX_DEVICES GPUs (the scene replicated on each, the frame split
+ * into row stripes and gathered on the first device over RCCL); it is not re-entrant.
+ * Every call restores the calling thread's current HIP device before it returns.
  */
 #ifndef RT_AMD_H
 #define RT_AMD_H
@@ -30,8 +32,11 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3   /* 2: rt_config_desc gained scatter_seed / scatter_mode;
-                              3: image textures (rt_image_desc, rt_shade.image, sky_image) */
+#define RT_ABI_VERSION 4   /* 2: rt_config_desc gained scatter_seed / scatter_mode;
+                              3: image textures (rt_image_desc, rt_shade.image, sky_image);
+                              4: multi-device contexts (rt_create_desc.devices), rt_trace_frame_device,
+                                 rt_frame_fault, rt_ctx_info */
+#define RT_MAX_DEVICES 8
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define RT_OK             0
@@ -180,9 +185,21 @@ typedef struct rt_stats {
 /* ---- context ------------------------------------------------------------------------------ */
 typedef struct rt_ctx rt_ctx;
 
+/* The GPUs of a context.  n_devices == 0: the one GPU `device`.  n_devices = N >= 1: devices[0..N-1]
+ * (devices[0] assembles frames).  Each device holds a replica of the scene and traces the row
+ * stripes of its part: rows are cut into stripes of `stripe_rows` (0: 8) and stripe s belongs to
+ * device s % N, which balances cost across the frame (sky rays cost more than hits).  The parts are
+ * gathered to devices[0] with one RCCL ncclGather per output array (ncclCommInitAll over the
+ * devices, in this process), de-interleaved there by one kernel, and copied to the host once.
+ * A device may be listed more than once (several parts on one GPU: the same code path, with the
+ * gather done by device copies, since RCCL admits one rank per GPU); RT_CREATE_PEER_GATHER selects
+ * device copies for distinct GPUs too. */
 typedef struct rt_create_desc {
-    int32_t device;       /* HIP device ordinal */
-    int32_t flags;        /* RT_CREATE_*        */
+    int32_t device;                   /* HIP device ordinal (n_devices == 0)          */
+    int32_t flags;                    /* RT_CREATE_*                                  */
+    int32_t n_devices;                /* 0, or the number of entries in devices[]     */
+    int32_t stripe_rows;              /* rows per stripe of the multi-device split; 0 = 8 */
+    int32_t devices[RT_MAX_DEVICES];  /* HIP device ordinals                          */
 } rt_create_desc;
 
 /* Disable the per-node cull hierarchies: every entity of a returned node runs the exact test
@@ -191,8 +208,23 @@ typedef struct rt_create_desc {
 /* Run each frame as one fused trace kernel instead of the walk pass + test pass (verification
  * mode; results are identical by construction). */
 #define RT_CREATE_NO_SPLIT 2
+/* Gather the parts of a multi-device frame with device-to-device copies (hipMemcpyPeerAsync over
+ * xGMI) instead of RCCL. */
+#define RT_CREATE_PEER_GATHER 4
 
 int  rt_create(const rt_create_desc *desc, rt_ctx **out);
+
+/* What a context runs on. */
+#define RT_GATHER_NONE 0   /* one part: the frame is traced in place on devices[0]      */
+#define RT_GATHER_RCCL 1   /* ncclGather of the parts to devices[0] (ncclScatter for blends) */
+#define RT_GATHER_PEER 2   /* hipMemcpyPeerAsync of the parts to devices[0]               */
+typedef struct rt_ctx_info {
+    int32_t n_devices;
+    int32_t devices[RT_MAX_DEVICES];
+    int32_t stripe_rows;
+    int32_t gather;                   /* RT_GATHER_*                                   */
+} rt_ctx_info;
+int  rt_ctx_info_get(const rt_ctx *ctx, rt_ctx_info *out);
 void rt_destroy(rt_ctx *ctx);
 const char *rt_last_error(void);
 int  rt_abi_version(void);
@@ -227,12 +259,16 @@ int  rt_update_scene(rt_ctx *ctx, const rt_scene_desc *scene, rt_update_stats *s
 /* Full frame, host buffers.  rgb_inout is the ExposureBuffer's Float32Array (W*H*3, row-major,
  * interleaved RGB); it is read (when col_weight != 1) and written.  hit_entity / hit_node
  * (W*H int32, nullable) receive the entity id / DFS node id of the primary collision, -1 for none.
- * status (W*H uint8, nullable): 0 ok, 1 acute-normal warning, 2 fault, 3 step cap. */
+ * status (W*H uint8, nullable): 0 ok, 1 acute-normal warning, 2 fault, 3 step cap.
+ * On a multi-device context every device traces its stripes and the frame is assembled on
+ * devices[0] before the one copy back; stats sums the devices' counters (kernel_ms: the slowest
+ * device).  Synchronous, like the reference's trace_frame. */
 int  rt_trace_frame(rt_ctx *ctx, const rt_camera_desc *cam, const rt_config_desc *cfg,
                     float *rgb_inout, int32_t *hit_entity, int32_t *hit_node,
                     uint8_t *status, rt_stats *stats);
 
-/* Row-striped frame slice for multi-GPU: rows are grouped in stripes of `stripe_rows`; stripe s
+/* Row-striped frame slice for one rank of a multi-process split (one process per GPU, the frame
+ * gathered by the host program; bench.py under torchrun).  Single-device contexts only.  Rows are grouped in stripes of `stripe_rows`; stripe s
  * belongs to part (s % n_parts).  Writes this part's rows compactly (stripe order) into the
  * DEVICE buffer d_rgb (rows_of_part * W * 3 floats) on the HIP stream `stream` (NULL = the
  * context's stream) and returns without synchronising unless stats != NULL.  With col_weight != 1
@@ -242,6 +278,22 @@ int  rt_trace_frame(rt_ctx *ctx, const rt_camera_desc *cam, const rt_config_desc
 int  rt_trace_rows_device(rt_ctx *ctx, const rt_camera_desc *cam, const rt_config_desc *cfg,
                           int32_t part, int32_t n_parts, int32_t stripe_rows,
                           void *d_rgb, void *stream, int32_t *rows_out, rt_stats *stats);
+/* (Faults of this asynchronous path: rt_frame_fault.) */
+
+/* Full frame into DEVICE memory on devices[0]: d_rgb is W*H*3 floats (row-major interleaved RGB, the
+ * ExposureBuffer layout), read when col_weight != 1 (the blend of rt_trace_frame) and written.
+ * Asynchronous: work is ordered after what `stream` (a devices[0] stream; NULL = the context's
+ * own) has queued, and `stream` is ordered after the frame, so the caller may read d_rgb in stream
+ * order.  Any number of devices.  Frames in flight: use one context per frame in flight (a
+ * context's buffers are reused by its next frame in stream order).  Faults are reported by
+ * rt_frame_fault. */
+int  rt_trace_frame_device(rt_ctx *ctx, const rt_camera_desc *cam, const rt_config_desc *cfg, float *d_rgb,
+                           void *stream);
+
+/* Synchronises the context's streams; *fault = 1 when a ray of the last frame issued on the context
+ * (rt_trace_frame_device / rt_trace_rows_device) reached a reference throw (RT_E_FAULT of
+ * rt_trace_frame), else 0. */
+int  rt_frame_fault(rt_ctx *ctx, int32_t *fault);
 
 /* Kernel time (ms) of the last `n` trace-kernel launches issued by rt_trace_rows_device, oldest
  * first, measured with HIP events on the launch stream.  Synchronises.  Returns count written. */

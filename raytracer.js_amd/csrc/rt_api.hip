@@ -2,8 +2,9 @@
 //
 // rt_trace_frame replaces the body of Raytracer.trace_frame (src/raytracer.ts:308-330): the camera
 // state and RaytracerConfig arrive as plain structs, the scene was flattened once by
-// rt_upload_scene, the kernels run on this context's GPU, and the ExposureBuffer pixels come back
-// in the caller's Float32Array.  A ray that reaches a state where the reference throws a JS Error
+// rt_upload_scene, the kernels run on this context's GPUs (row stripes per GPU, gathered on the
+// first over RCCL: frame_multi), and the ExposureBuffer pixels come back in the caller's
+// Float32Array.  A ray that reaches a state where the reference throws a JS Error
 // makes the call return RT_E_FAULT (outputs still written, status[] = 2 for those pixels).
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
@@ -11,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <array>
 #include <chrono>
 #include <new>
 #include <vector>
@@ -44,7 +47,7 @@ namespace {
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
-    int ensure(size_t bytes)
+    int ensure(size_t bytes)     // on the calling thread's current device
     {
         if (bytes <= cap) return RT_OK;
         if (p) (void)hipFree(p);
@@ -63,10 +66,29 @@ struct DevBuf {
     }
 };
 
+// The calling thread's current device, restored when an entry point returns (a host such as torch
+// keeps its own notion of the current device on the same thread).
+struct DevGuard {
+    int prev = -1;
+    DevGuard() { if (hipGetDevice(&prev) != hipSuccess) prev = -1; }
+    ~DevGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+// Per-GPU state of a context: its stream, its replica of the scene, its frame buffers.
+struct RtDevice {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    RtDevScene scene{};
+    DevBuf b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters,
+        b_fault;
+    std::vector<std::array<hipEvent_t, 2>> ev;   // trace-kernel timing ring
+    int ev_next = 0, ev_count = 0;
+    hipEvent_t sync = nullptr;                   // cross-stream / cross-device ordering
+};
+
 }  // namespace
 
 struct rt_ctx {
-    int device = 0;
     int flags = 0;
     bool bvh_sah = true;             // SAH splits (RT_BVH_SAH=0: median split)
     bool split = true;               // walk pass + test pass (RT_SPLIT=0: fused k_trace)
@@ -75,40 +97,70 @@ struct rt_ctx {
     int claim_chunk = 1;             // items per queue claim in the short passes (RT_CLAIM_CHUNK)
     int xcd_mask = 0;                // passes claiming per-XCD bands (RT_XCD: 1 walk, 2 first, 4 shade)
     int shade_occ = 3;               // k_shade occupancy variant (RT_SHADE_OCC)
-    int cont_group = 8;              // continuation rays per wave (RT_CONT_GROUP): their passes are
-                                     // latency-bound, fewer lanes per wave shorten the slowest wave
+    int cont_group = 8;              // continuation rays per wave (RT_CONT_GROUP, a power of two <= 64):
+                                     // their passes are latency-bound, fewer lanes per wave shorten the
+                                     // slowest wave
     int seg = 8;                     // segments per bounce ray, levels >= 1 (RT_SEG: 0/1 off, 2..64)
     int occ = 0;
     int diag = 0;
-    hipStream_t stream = nullptr;
     bool has_scene = false;
     bool scatter = false;            // a mirror shade with roughness > 0 is reachable
-    RtDevScene scene{};
-    RtSceneStore *store = nullptr;   // the resident scene (rt_scene.hip)
-    DevBuf b_stat, b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters, b_fault;
-    DevBuf b_walk;
-    static constexpr int NEV = 256;
-    hipEvent_t ev[NEV][2] = {};
-    int ev_next = 0, ev_count = 0;
+    RtSceneStore *store = nullptr;   // the resident scene (rt_scene.hip), replicated on every device
+    int n_dev = 1;
+    RtDevice dev[RT_MAX_DEVICES];
+    int stripe = 8;                  // rows per stripe of the multi-device split
+    int gather = RT_GATHER_NONE;     // how parts reach dev[0]
+    void *comm[RT_MAX_DEVICES] = {}; // RCCL communicators (ncclCommInitAll), one per device
+    // on dev[0]: the stacked parts (gather target) and, for host-buffer frames, the assembled frame
+    DevBuf g_stack, g_frame, g_hit_e, g_hit_n, g_status;
+    DevBuf b_stat, b_walk;           // exposure statistics, debug walks (dev[0])
 };
 
-static int use_device(rt_ctx *c)
+static int use_device(const RtDevice &d)
 {
-    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipSetDevice(d.device));
     return RT_OK;
+}
+
+static int rccl_try(int rc, const char *what)
+{
+    if (rc == 0) return RT_OK;
+    const RtRccl *R = rt_rccl();
+    return rt_set_error(RT_E_HIP, "%s: RCCL error %d (%s)", what, rc, R ? R->error_string(rc) : "?");
+}
+
+static int pow2_at_most_64(int v)
+{
+    int k = 1;
+    while (k < 64 && 2 * k <= v) k *= 2;
+    return k;
 }
 
 extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
 {
     if (!out) return rt_set_error(RT_E_INVALID, "rt_create: out is null");
     *out = nullptr;
+    DevGuard guard;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return rt_set_error(RT_E_NODEVICE, "rt_create: no HIP device");
-    const int dev = desc ? desc->device : 0;
-    if (dev < 0 || dev >= n) return rt_set_error(RT_E_INVALID, "rt_create: device %d of %d", dev, n);
+    int devs[RT_MAX_DEVICES];
+    int nd = 1;
+    if (desc && desc->n_devices != 0) {
+        if (desc->n_devices < 0 || desc->n_devices > RT_MAX_DEVICES)
+            return rt_set_error(RT_E_INVALID, "rt_create: n_devices %d (1..%d)", desc->n_devices, RT_MAX_DEVICES);
+        nd = desc->n_devices;
+        for (int k = 0; k < nd; k++) devs[k] = desc->devices[k];
+    } else {
+        devs[0] = desc ? desc->device : 0;
+    }
+    for (int k = 0; k < nd; k++)
+        if (devs[k] < 0 || devs[k] >= n) return rt_set_error(RT_E_NODEVICE, "rt_create: device %d of %d", devs[k], n);
+    if (desc && desc->stripe_rows < 0) return rt_set_error(RT_E_INVALID, "rt_create: stripe_rows %d", desc->stripe_rows);
     rt_ctx *c = new (std::nothrow) rt_ctx();
     if (!c) return rt_set_error(RT_E_INVALID, "rt_create: out of memory");
-    c->device = dev;
+    c->n_dev = nd;
+    for (int k = 0; k < nd; k++) c->dev[k].device = devs[k];
+    c->stripe = desc && desc->stripe_rows > 0 ? desc->stripe_rows : 8;
     c->flags = desc ? desc->flags : 0;
     if (const char *e = getenv("RT_NO_CULL"))
         if (e[0] == '1') c->flags |= RT_CREATE_NO_CULL;
@@ -120,25 +172,58 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_SHADE_OCC")) c->shade_occ = atoi(e);
     if (const char *e = getenv("RT_CLAIM_CHUNK")) c->claim_chunk = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_SPLIT_LEVELS")) c->split_levels = atoi(e) < 1 ? 1 : atoi(e);
-    if (const char *e = getenv("RT_CONT_GROUP")) c->cont_group = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
-    if (const char *e = getenv("RT_SEG")) {
-        int k = 1;
-        while (k < 64 && 2 * k <= atoi(e)) k *= 2;                  // a power of two, at most 64
-        c->seg = atoi(e) > 1 ? k : 0;
-    }
+    if (const char *e = getenv("RT_CONT_GROUP")) c->cont_group = pow2_at_most_64(atoi(e));
+    if (const char *e = getenv("RT_SEG")) c->seg = atoi(e) > 1 ? pow2_at_most_64(atoi(e)) : 0;
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
-    int r = use_device(c);
-    if (r == RT_OK && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
-        r = rt_set_error(RT_E_HIP, "rt_create: hipStreamCreate failed");
-    for (int i = 0; r == RT_OK && i < rt_ctx::NEV; i++)
-        if (hipEventCreate(&c->ev[i][0]) != hipSuccess || hipEventCreate(&c->ev[i][1]) != hipSuccess)
+    // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
+    // parts on one GPU) gathers by device copies, as RT_CREATE_PEER_GATHER asks for.  RT_GATHER
+    // (rccl / peer) forces a mode, also for one device (tests on a one-GPU host).
+    bool distinct = true;
+    for (int a = 0; a < nd; a++)
+        for (int b = a + 1; b < nd; b++) distinct = distinct && devs[a] != devs[b];
+    c->gather = nd == 1 ? RT_GATHER_NONE : (distinct && !(c->flags & RT_CREATE_PEER_GATHER) ? RT_GATHER_RCCL : RT_GATHER_PEER);
+    if (const char *e = getenv("RT_GATHER")) {
+        if (!strcmp(e, "rccl") && distinct) c->gather = RT_GATHER_RCCL;
+        if (!strcmp(e, "peer")) c->gather = RT_GATHER_PEER;
+    }
+    int r = RT_OK;
+    void *streams[RT_MAX_DEVICES];
+    for (int k = 0; r == RT_OK && k < nd; k++) {
+        RtDevice &d = c->dev[k];
+        r = use_device(d);
+        if (r == RT_OK && hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess)
+            r = rt_set_error(RT_E_HIP, "rt_create: hipStreamCreate failed");
+        d.ev.assign(k == 0 ? 256 : 16, {nullptr, nullptr});
+        for (auto &e : d.ev)
+            if (r == RT_OK && (hipEventCreate(&e[0]) != hipSuccess || hipEventCreate(&e[1]) != hipSuccess))
+                r = rt_set_error(RT_E_HIP, "rt_create: hipEventCreate failed");
+        if (r == RT_OK && hipEventCreateWithFlags(&d.sync, hipEventDisableTiming) != hipSuccess)
             r = rt_set_error(RT_E_HIP, "rt_create: hipEventCreate failed");
-    if (r == RT_OK && !(c->store = rt_store_new(c->bvh_sah))) r = rt_set_error(RT_E_INVALID, "rt_create: out of memory");
-    if (r == RT_OK) r = c->b_setup.ensure(sizeof(RtFrameSetup));
-    if (r == RT_OK) r = c->b_counters.ensure(sizeof(unsigned long long) * CT_N);
-    if (r == RT_OK) r = c->b_fault.ensure(sizeof(int));   // ray fault flag
-    if (r == RT_OK) r = c->b_ctr.ensure(sizeof(int32_t) * RT_CTR_INTS);
+        if (r == RT_OK) r = d.b_setup.ensure(sizeof(RtFrameSetup));
+        if (r == RT_OK) r = d.b_counters.ensure(sizeof(unsigned long long) * CT_N);
+        if (r == RT_OK) r = d.b_fault.ensure(sizeof(int));   // ray fault flag
+        if (r == RT_OK) r = d.b_ctr.ensure(sizeof(int32_t) * RT_CTR_INTS);
+        if (r == RT_OK) HIP_TRY(hipMemsetAsync(d.b_fault.p, 0, sizeof(int), d.stream));
+        streams[k] = d.stream;
+        // peer access between dev[0] and the others (the peer gather; RCCL sets up its own)
+        if (r == RT_OK && k > 0 && d.device != devs[0]) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, d.device, devs[0]) == hipSuccess && can)
+                (void)hipDeviceEnablePeerAccess(devs[0], 0);
+            (void)hipSetDevice(devs[0]);
+            if (hipDeviceCanAccessPeer(&can, devs[0], d.device) == hipSuccess && can)
+                (void)hipDeviceEnablePeerAccess(d.device, 0);
+            (void)hipGetLastError();            // "already enabled" is not an error here
+        }
+    }
+    if (r == RT_OK && c->gather == RT_GATHER_RCCL) {
+        const RtRccl *R = rt_rccl();
+        if (!R) r = rt_set_error(RT_E_HIP, "rt_create: %s (RT_CREATE_PEER_GATHER gathers without RCCL)", rt_rccl_error());
+        else r = rccl_try(R->comm_init_all(c->comm, nd, devs), "ncclCommInitAll");
+    }
+    if (r == RT_OK && !(c->store = rt_store_new(c->bvh_sah, nd, devs, streams)))
+        r = rt_set_error(RT_E_INVALID, "rt_create: out of memory");
     if (r != RT_OK) {
         rt_destroy(c);
         return r;
@@ -150,41 +235,69 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
 extern "C" void rt_destroy(rt_ctx *c)
 {
     if (!c) return;
-    (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevGuard guard;
+    for (int k = 0; k < c->n_dev; k++) {
+        (void)hipSetDevice(c->dev[k].device);
+        if (c->dev[k].stream) (void)hipStreamSynchronize(c->dev[k].stream);
+    }
+    if (c->gather == RT_GATHER_RCCL) {
+        const RtRccl *R = rt_rccl();
+        for (int k = 0; R && k < c->n_dev; k++)
+            if (c->comm[k]) (void)R->comm_destroy(c->comm[k]);
+    }
     rt_store_free(c->store);
     c->store = nullptr;
-    DevBuf *bufs[] = {&c->b_stat, &c->b_cand, &c->b_cand_n, &c->b_first, &c->b_queue, &c->b_ctr, &c->b_setup, &c->b_dirs,
-                      &c->b_rgb, &c->b_hit_e, &c->b_hit_n, &c->b_status, &c->b_counters, &c->b_fault,
-                      &c->b_walk};
-    for (DevBuf *b : bufs) b->release();
-    for (int i = 0; i < rt_ctx::NEV; i++)
-        for (int k = 0; k < 2; k++)
-            if (c->ev[i][k]) (void)hipEventDestroy(c->ev[i][k]);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    (void)hipSetDevice(c->dev[0].device);
+    for (DevBuf *b : {&c->g_stack, &c->g_frame, &c->g_hit_e, &c->g_hit_n, &c->g_status, &c->b_stat, &c->b_walk})
+        b->release();
+    for (int k = 0; k < c->n_dev; k++) {
+        RtDevice &d = c->dev[k];
+        (void)hipSetDevice(d.device);
+        for (DevBuf *b : {&d.b_cand, &d.b_cand_n, &d.b_first, &d.b_queue, &d.b_ctr, &d.b_setup, &d.b_dirs, &d.b_rgb,
+                          &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault})
+            b->release();
+        for (auto &e : d.ev)
+            for (hipEvent_t x : e)
+                if (x) (void)hipEventDestroy(x);
+        if (d.sync) (void)hipEventDestroy(d.sync);
+        if (d.stream) (void)hipStreamDestroy(d.stream);
+    }
     delete c;
+}
+
+extern "C" int rt_ctx_info_get(const rt_ctx *c, rt_ctx_info *out)
+{
+    if (!c || !out) return rt_set_error(RT_E_INVALID, "rt_ctx_info_get: null argument");
+    memset(out, 0, sizeof *out);
+    out->n_devices = c->n_dev;
+    for (int k = 0; k < c->n_dev; k++) out->devices[k] = c->dev[k].device;
+    out->stripe_rows = c->stripe;
+    out->gather = c->gather;
+    return RT_OK;
+}
+
+static int upload(rt_ctx *c, const rt_scene_desc *s, bool incremental, rt_update_stats *stats)
+{
+    DevGuard guard;
+    c->has_scene = false;
+    RtDevScene scenes[RT_MAX_DEVICES];
+    int r = rt_store_upload(c->store, s, incremental, scenes, &c->scatter, stats);
+    if (r != RT_OK) return r;
+    for (int k = 0; k < c->n_dev; k++) c->dev[k].scene = scenes[k];
+    c->has_scene = true;
+    return RT_OK;
 }
 
 extern "C" int rt_upload_scene(rt_ctx *c, const rt_scene_desc *s)
 {
     if (!c || !s) return rt_set_error(RT_E_INVALID, "rt_upload_scene: null argument");
-    int r = use_device(c);
-    if (r != RT_OK) return r;
-    c->has_scene = false;
-    if ((r = rt_store_upload(c->store, s, false, c->stream, &c->scene, &c->scatter, nullptr)) != RT_OK) return r;
-    c->has_scene = true;
-    return RT_OK;
+    return upload(c, s, false, nullptr);
 }
 
 extern "C" int rt_update_scene(rt_ctx *c, const rt_scene_desc *s, rt_update_stats *stats)
 {
     if (!c || !s) return rt_set_error(RT_E_INVALID, "rt_update_scene: null argument");
-    int r = use_device(c);
-    if (r != RT_OK) return r;
-    c->has_scene = false;
-    if ((r = rt_store_upload(c->store, s, true, c->stream, &c->scene, &c->scatter, stats)) != RT_OK) return r;
-    c->has_scene = true;
-    return RT_OK;
+    return upload(c, s, true, stats);
 }
 
 static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg)
@@ -193,10 +306,11 @@ static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_confi
     if (!c->has_scene) return rt_set_error(RT_E_NOSCENE, "no scene uploaded");
     if (cam->width <= 0 || cam->height <= 0 || (long long)cam->width * cam->height > (1ll << 31) / 3)
         return rt_set_error(RT_E_INVALID, "bad screen size %dx%d", cam->width, cam->height);
-    if (cfg->default_substance < -1 || cfg->default_substance >= c->scene.n_subs)
+    const RtDevScene &S = c->dev[0].scene;
+    if (cfg->default_substance < -1 || cfg->default_substance >= S.n_subs)
         return rt_set_error(RT_E_INVALID, "bad default_substance %d", cfg->default_substance);
-    if (cfg->sky_image < 0 || cfg->sky_image > c->scene.n_images)
-        return rt_set_error(RT_E_INVALID, "bad sky_image %d (%d images)", cfg->sky_image, c->scene.n_images);
+    if (cfg->sky_image < 0 || cfg->sky_image > S.n_images)
+        return rt_set_error(RT_E_INVALID, "bad sky_image %d (%d images)", cfg->sky_image, S.n_images);
     if (cfg->scatter_mode != RT_SCATTER_REJECT && cfg->scatter_mode != RT_SCATTER_COUNTER)
         return rt_set_error(RT_E_INVALID, "bad scatter_mode %d", cfg->scatter_mode);
     if (c->scatter && cfg->scatter_mode != RT_SCATTER_COUNTER)
@@ -207,35 +321,36 @@ static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_confi
     return RT_OK;
 }
 
-// Prepare per-frame buffers and the launch description for one part.
-static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, int part, int n_parts,
-                   int stripe, bool want_ids, RtLaunch &L)
+// Per-frame buffers of device d and the launch description of one part.  The part's outputs go to
+// d.b_rgb / d.b_hit_* unless the caller repoints L.rgb.  Device d must be current.
+static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_config_desc *cfg, int part,
+                   int n_parts, int stripe, bool want_ids, RtLaunch &L)
 {
     const int rows = rt_part_rows(cam->height, part, n_parts, stripe);
     const size_t P = (size_t)rows * (size_t)cam->width;
     int r;
-    if ((r = c->b_dirs.ensure(sizeof(double) * 3 * (P ? P : 1))) != RT_OK) return r;
+    if ((r = d.b_dirs.ensure(sizeof(double) * 3 * (P ? P : 1))) != RT_OK) return r;
     if (want_ids) {
-        if ((r = c->b_hit_e.ensure(sizeof(int32_t) * (P ? P : 1))) != RT_OK) return r;
-        if ((r = c->b_hit_n.ensure(sizeof(int32_t) * (P ? P : 1))) != RT_OK) return r;
-        if ((r = c->b_status.ensure(P ? P : 1)) != RT_OK) return r;
+        if ((r = d.b_hit_e.ensure(sizeof(int32_t) * (P ? P : 1))) != RT_OK) return r;
+        if ((r = d.b_hit_n.ensure(sizeof(int32_t) * (P ? P : 1))) != RT_OK) return r;
+        if ((r = d.b_status.ensure(P ? P : 1)) != RT_OK) return r;
     }
     memset(&L, 0, sizeof L);
-    L.scene = c->scene;
+    L.scene = d.scene;
     L.cam = *cam;
     L.cfg = *cfg;
     L.part = part;
     L.n_parts = n_parts;
     L.stripe_rows = stripe;
     L.rows = rows;
-    L.setup = (RtFrameSetup *)c->b_setup.p;
-    L.dirs = (double *)c->b_dirs.p;
-    L.hit_entity = want_ids ? (int32_t *)c->b_hit_e.p : nullptr;
-    L.hit_node = want_ids ? (int32_t *)c->b_hit_n.p : nullptr;
-    L.status = want_ids ? (uint8_t *)c->b_status.p : nullptr;
-    L.fault = (int32_t *)c->b_fault.p;
+    L.setup = (RtFrameSetup *)d.b_setup.p;
+    L.dirs = (double *)d.b_dirs.p;
+    L.hit_entity = want_ids ? (int32_t *)d.b_hit_e.p : nullptr;
+    L.hit_node = want_ids ? (int32_t *)d.b_hit_n.p : nullptr;
+    L.status = want_ids ? (uint8_t *)d.b_status.p : nullptr;
+    L.fault = (int32_t *)d.b_fault.p;
     L.cull = (c->flags & RT_CREATE_NO_CULL) ? 0 : 1;
-    L.ctr = (int32_t *)c->b_ctr.p;
+    L.ctr = (int32_t *)d.b_ctr.p;
     L.occ = c->occ;
     L.diag = c->diag;
     L.cont_group = c->cont_group;
@@ -244,18 +359,19 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
     L.xcd_mask = c->xcd_mask;
     L.shade_occ = c->shade_occ;
     L.seg = c->seg;
+    L.blend = cfg->col_weight != 1.0;
     if (c->split && P > 0) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).
         L.cand_cap = c->cand_cap;
-        if (c->b_cand.ensure(sizeof(int32_t) * (size_t)L.cand_cap * P) == RT_OK &&
-            c->b_cand_n.ensure(2 * sizeof(int32_t) * P) == RT_OK && c->b_first.ensure(2 * sizeof(int32_t) * P) == RT_OK &&
-            c->b_queue.ensure(3 * sizeof(RtCont) * P) == RT_OK) {
-            L.cand = (int32_t *)c->b_cand.p;
-            L.cand_n = (int32_t *)c->b_cand_n.p;
+        if (d.b_cand.ensure(sizeof(int32_t) * (size_t)L.cand_cap * P) == RT_OK &&
+            d.b_cand_n.ensure(2 * sizeof(int32_t) * P) == RT_OK && d.b_first.ensure(2 * sizeof(int32_t) * P) == RT_OK &&
+            d.b_queue.ensure(3 * sizeof(RtCont) * P) == RT_OK) {
+            L.cand = (int32_t *)d.b_cand.p;
+            L.cand_n = (int32_t *)d.b_cand_n.p;
             L.ray_cn = L.cand_n + P;
-            L.first = (int32_t *)c->b_first.p;
-            L.queue[0] = (RtCont *)c->b_queue.p;
+            L.first = (int32_t *)d.b_first.p;
+            L.queue[0] = (RtCont *)d.b_queue.p;
             L.queue[1] = L.queue[0] + P;
             L.ovf = L.queue[1] + P;
         } else {
@@ -270,11 +386,202 @@ static int prepare(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *c
 
 static void fill_stats(rt_stats *st, const unsigned long long *h)
 {
-    st->segments = (int64_t)h[CT_SEG]; st->n_ret = (int64_t)h[CT_RET]; st->n_slot = (int64_t)h[CT_SLOT];
-    st->n_loc = (int64_t)h[CT_LOC]; st->n_sph = (int64_t)h[CT_SPH]; st->n_box = (int64_t)h[CT_BOX];
-    st->n_tri = (int64_t)h[CT_TRI]; st->n_hit = (int64_t)h[CT_HIT]; st->primary = (int64_t)h[CT_PRIM];
-    st->n_warn = (int64_t)h[CT_WARN]; st->n_fault = (int64_t)h[CT_FAULT];
-    st->n_cull = (int64_t)h[CT_CULL]; st->n_exact = (int64_t)h[CT_EXACT];
+    st->segments += (int64_t)h[CT_SEG]; st->n_ret += (int64_t)h[CT_RET]; st->n_slot += (int64_t)h[CT_SLOT];
+    st->n_loc += (int64_t)h[CT_LOC]; st->n_sph += (int64_t)h[CT_SPH]; st->n_box += (int64_t)h[CT_BOX];
+    st->n_tri += (int64_t)h[CT_TRI]; st->n_hit += (int64_t)h[CT_HIT]; st->primary += (int64_t)h[CT_PRIM];
+    st->n_warn += (int64_t)h[CT_WARN]; st->n_fault += (int64_t)h[CT_FAULT];
+    st->n_cull += (int64_t)h[CT_CULL]; st->n_exact += (int64_t)h[CT_EXACT];
+}
+
+static hipEvent_t *next_events(RtDevice &d)
+{
+    hipEvent_t *ev = d.ev[d.ev_next].data();
+    d.ev_next = (d.ev_next + 1) % (int)d.ev.size();
+    d.ev_count = d.ev_count < (int)d.ev.size() ? d.ev_count + 1 : (int)d.ev.size();
+    return ev;
+}
+
+// `waiter` (a stream of device dw) waits for everything queued so far on device ds's stream.
+static int order_after(RtDevice &src, hipStream_t waiter)
+{
+    HIP_TRY(hipSetDevice(src.device));
+    HIP_TRY(hipEventRecord(src.sync, src.stream));
+    HIP_TRY(hipStreamWaitEvent(waiter, src.sync, 0));
+    return RT_OK;
+}
+
+// Outputs of a whole frame on dev[0] (each nullable but rgb).
+struct FrameOut {
+    float *rgb;
+    int32_t *hit_e, *hit_n;
+    uint8_t *status;
+};
+
+// One frame over every device of the context, assembled on dev[0] into `o`:
+//   blend:  dev[0] deals the current frame out into stacked parts (k_stripes) and scatters them
+//           (ncclScatter / peer copies) into each device's part buffer;
+//   trace:  each device runs the frame's kernels over its stripes into its part buffers;
+//   gather: ncclGather of each output array to dev[0]'s stack (one group), or peer copies;
+//   dev[0]: k_stripes de-interleaves the stack into the frame.
+// Everything is queued on the devices' streams; dev[0]'s stream is ordered after `caller` first
+// and `caller` after the frame (when given).  Returns with the work queued.
+static int frame_multi(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, const FrameOut &o,
+                       hipStream_t caller, bool stats)
+{
+    const int N = c->n_dev, H = cam->height, W = cam->width, stripe = c->stripe;
+    const bool ids = o.hit_e || o.hit_n || o.status;
+    int max_rows = 0;
+    for (int p = 0; p < N; p++) max_rows = std::max(max_rows, rt_part_rows(H, p, N, stripe));
+    const size_t PS = (size_t)max_rows * (size_t)W;          // pixels per part buffer
+    RtDevice &d0 = c->dev[0];
+    int r;
+    // stacked parts on dev[0]: rgb | hit_e | hit_n | status
+    HIP_TRY(hipSetDevice(d0.device));
+    const size_t st_rgb = (size_t)N * PS * 12, st_ids = ids ? (size_t)N * PS * 9 : 0;
+    if ((r = c->g_stack.ensure(st_rgb + st_ids + 16)) != RT_OK) return r;
+    uint8_t *stack = (uint8_t *)c->g_stack.p;
+    float *stack_rgb = (float *)stack;
+    int32_t *stack_he = (int32_t *)(stack + st_rgb);
+    int32_t *stack_hn = stack_he + (size_t)N * PS;
+    uint8_t *stack_st = (uint8_t *)(stack_hn + (size_t)N * PS);
+    if (caller && caller != d0.stream) {
+        HIP_TRY(hipEventRecord(d0.sync, caller));
+        HIP_TRY(hipStreamWaitEvent(d0.stream, d0.sync, 0));
+    }
+    const bool blend = cfg->col_weight != 1.0;
+    // per-device part buffers (every device's buffer is PS pixels: the gather sends equal counts)
+    RtLaunch L[RT_MAX_DEVICES];
+    for (int k = 0; k < N; k++) {
+        RtDevice &d = c->dev[k];
+        if ((r = use_device(d)) != RT_OK) return r;
+        if ((r = d.b_rgb.ensure(sizeof(float) * 3 * PS)) != RT_OK) return r;
+        if ((r = prepare(c, d, cam, cfg, k, N, stripe, ids, L[k])) != RT_OK) return r;
+        if (ids) {   // the gathered id arrays are PS long on every device
+            if ((r = d.b_hit_e.ensure(sizeof(int32_t) * PS)) != RT_OK) return r;
+            if ((r = d.b_hit_n.ensure(sizeof(int32_t) * PS)) != RT_OK) return r;
+            if ((r = d.b_status.ensure(PS)) != RT_OK) return r;
+            L[k].hit_entity = (int32_t *)d.b_hit_e.p;
+            L[k].hit_node = (int32_t *)d.b_hit_n.p;
+            L[k].status = (uint8_t *)d.b_status.p;
+        }
+        L[k].rgb = (float *)d.b_rgb.p;
+        HIP_TRY(hipMemsetAsync(d.b_fault.p, 0, sizeof(int), d.stream));
+        if (stats) {
+            HIP_TRY(hipMemsetAsync(d.b_counters.p, 0, sizeof(unsigned long long) * CT_N, d.stream));
+            L[k].counters = (unsigned long long *)d.b_counters.p;
+        }
+    }
+    const RtRccl *R = c->gather == RT_GATHER_RCCL ? rt_rccl() : nullptr;
+    if (c->gather == RT_GATHER_RCCL && !R) return rt_set_error(RT_E_HIP, "RCCL unavailable: %s", rt_rccl_error());
+    if (blend) {
+        HIP_TRY(hipSetDevice(d0.device));
+        if ((r = rt_launch_stripes(o.rgb, stack_rgb, H, N, stripe, max_rows, (size_t)W * 12, 0, d0.stream)) != RT_OK)
+            return r;
+        if (R) {
+            if ((r = rccl_try(R->group_start(), "ncclGroupStart")) != RT_OK) return r;
+            for (int k = 0; k < N; k++)
+                if ((r = rccl_try(R->scatter(stack_rgb, c->dev[k].b_rgb.p, PS * 3, RT_NCCL_FLOAT32, 0, c->comm[k],
+                                             c->dev[k].stream), "ncclScatter")) != RT_OK) {
+                    (void)R->group_end();
+                    return r;
+                }
+            if ((r = rccl_try(R->group_end(), "ncclGroupEnd")) != RT_OK) return r;
+        } else {
+            for (int k = 0; k < N; k++)
+                HIP_TRY(hipMemcpyPeerAsync(c->dev[k].b_rgb.p, c->dev[k].device, stack_rgb + (size_t)k * PS * 3,
+                                           d0.device, sizeof(float) * 3 * PS, d0.stream));
+            for (int k = 1; k < N; k++)
+                if ((r = order_after(d0, c->dev[k].stream)) != RT_OK) return r;
+        }
+    }
+    for (int k = 0; k < N; k++) {
+        RtDevice &d = c->dev[k];
+        if ((r = use_device(d)) != RT_OK) return r;
+        hipEvent_t *ev = next_events(d);
+        if ((r = rt_launch_frame(L[k], d.stream, ev[0], ev[1])) != RT_OK) return r;
+    }
+    struct Arr { void *dev_buf[RT_MAX_DEVICES]; void *stack; size_t count, elem; int dtype; };
+    Arr arrs[4];
+    int n_arr = 0;
+    arrs[n_arr] = {{}, stack_rgb, PS * 3, 4, RT_NCCL_FLOAT32};
+    for (int k = 0; k < N; k++) arrs[n_arr].dev_buf[k] = c->dev[k].b_rgb.p;
+    n_arr++;
+    if (ids) {
+        arrs[n_arr] = {{}, stack_he, PS, 4, RT_NCCL_INT32};
+        for (int k = 0; k < N; k++) arrs[n_arr].dev_buf[k] = c->dev[k].b_hit_e.p;
+        n_arr++;
+        arrs[n_arr] = {{}, stack_hn, PS, 4, RT_NCCL_INT32};
+        for (int k = 0; k < N; k++) arrs[n_arr].dev_buf[k] = c->dev[k].b_hit_n.p;
+        n_arr++;
+        arrs[n_arr] = {{}, stack_st, PS, 1, RT_NCCL_UINT8};
+        for (int k = 0; k < N; k++) arrs[n_arr].dev_buf[k] = c->dev[k].b_status.p;
+        n_arr++;
+    }
+    if (R) {
+        if ((r = rccl_try(R->group_start(), "ncclGroupStart")) != RT_OK) return r;
+        for (int a = 0; a < n_arr; a++)
+            for (int k = 0; k < N; k++)
+                if ((r = rccl_try(R->gather(arrs[a].dev_buf[k], arrs[a].stack, arrs[a].count, arrs[a].dtype, 0,
+                                            c->comm[k], c->dev[k].stream), "ncclGather")) != RT_OK) {
+                    (void)R->group_end();
+                    return r;
+                }
+        if ((r = rccl_try(R->group_end(), "ncclGroupEnd")) != RT_OK) return r;
+    } else {
+        for (int k = 1; k < N; k++)
+            if ((r = order_after(c->dev[k], d0.stream)) != RT_OK) return r;
+        HIP_TRY(hipSetDevice(d0.device));
+        for (int a = 0; a < n_arr; a++)
+            for (int k = 0; k < N; k++)
+                HIP_TRY(hipMemcpyPeerAsync((uint8_t *)arrs[a].stack + (size_t)k * arrs[a].count * arrs[a].elem,
+                                           d0.device, arrs[a].dev_buf[k], c->dev[k].device,
+                                           arrs[a].count * arrs[a].elem, d0.stream));
+        // a device's next frame rewrites its part buffers only after dev[0] has copied them
+        for (int k = 1; k < N; k++)
+            if ((r = order_after(d0, c->dev[k].stream)) != RT_OK) return r;
+    }
+    HIP_TRY(hipSetDevice(d0.device));
+    if ((r = rt_launch_stripes(stack_rgb, o.rgb, H, N, stripe, max_rows, (size_t)W * 12, 1, d0.stream)) != RT_OK)
+        return r;
+    if (o.hit_e && (r = rt_launch_stripes(stack_he, o.hit_e, H, N, stripe, max_rows, (size_t)W * 4, 1, d0.stream)))
+        return r;
+    if (o.hit_n && (r = rt_launch_stripes(stack_hn, o.hit_n, H, N, stripe, max_rows, (size_t)W * 4, 1, d0.stream)))
+        return r;
+    if (o.status && (r = rt_launch_stripes(stack_st, o.status, H, N, stripe, max_rows, (size_t)W, 1, d0.stream)))
+        return r;
+    if (caller && caller != d0.stream) {
+        HIP_TRY(hipEventRecord(d0.sync, d0.stream));
+        HIP_TRY(hipStreamWaitEvent(caller, d0.sync, 0));
+    }
+    return RT_OK;
+}
+
+// After the frame's work is queued: wait for every device, OR the fault flags, sum the counters.
+static int finish(rt_ctx *c, int fault_dev0_read, rt_stats *stats, std::chrono::steady_clock::time_point t0,
+                  int *fault_out)
+{
+    int fault = fault_dev0_read;
+    if (stats) memset(stats, 0, sizeof *stats);
+    for (int k = 0; k < c->n_dev; k++) {
+        RtDevice &d = c->dev[k];
+        HIP_TRY(hipSetDevice(d.device));
+        int f = 0;
+        unsigned long long h[CT_N] = {};
+        HIP_TRY(hipMemcpyAsync(&f, d.b_fault.p, sizeof(int), hipMemcpyDeviceToHost, d.stream));
+        if (stats) HIP_TRY(hipMemcpyAsync(h, d.b_counters.p, sizeof h, hipMemcpyDeviceToHost, d.stream));
+        HIP_TRY(hipStreamSynchronize(d.stream));
+        fault |= f;
+        if (stats) {
+            fill_stats(stats, h);
+            const int last = ((d.ev_next - 1) % (int)d.ev.size() + (int)d.ev.size()) % (int)d.ev.size();
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, d.ev[last][0], d.ev[last][1]) != hipSuccess) (void)hipGetLastError();
+            stats->kernel_ms = std::max(stats->kernel_ms, (double)ms);
+        }
+    }
+    if (stats) stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    *fault_out = fault;
+    return RT_OK;
 }
 
 extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,
@@ -284,42 +591,87 @@ extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     int r = check_frame_args(c, cam, cfg);
     if (r != RT_OK) return r;
     if (!rgb_inout) return rt_set_error(RT_E_INVALID, "rt_trace_frame: rgb_inout is null");
-    if ((r = use_device(c)) != RT_OK) return r;
+    DevGuard guard;
+    RtDevice &d0 = c->dev[0];
+    if ((r = use_device(d0)) != RT_OK) return r;
     const int H = cam->height;
     const bool ids = hit_entity || hit_node || status;
-    RtLaunch L;
-    if ((r = prepare(c, cam, cfg, 0, 1, H, ids, L)) != RT_OK) return r;
     const size_t P = (size_t)cam->width * (size_t)H;
-    if ((r = c->b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
-    L.rgb = (float *)c->b_rgb.p;
-    L.blend = cfg->col_weight != 1.0;
-    if (L.blend) HIP_TRY(hipMemcpyAsync(L.rgb, rgb_inout, sizeof(float) * 3 * P, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(c->b_fault.p, 0, sizeof(int), c->stream));
-    if (stats) {
-        HIP_TRY(hipMemsetAsync(c->b_counters.p, 0, sizeof(unsigned long long) * CT_N, c->stream));
-        L.counters = (unsigned long long *)c->b_counters.p;
+    const bool blend = cfg->col_weight != 1.0;
+    FrameOut o = {};
+    if (c->gather == RT_GATHER_NONE) {
+        RtLaunch L;
+        if ((r = prepare(c, d0, cam, cfg, 0, 1, H, ids, L)) != RT_OK) return r;
+        if ((r = d0.b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
+        L.rgb = (float *)d0.b_rgb.p;
+        if (blend) HIP_TRY(hipMemcpyAsync(L.rgb, rgb_inout, sizeof(float) * 3 * P, hipMemcpyHostToDevice, d0.stream));
+        HIP_TRY(hipMemsetAsync(d0.b_fault.p, 0, sizeof(int), d0.stream));
+        if (stats) {
+            HIP_TRY(hipMemsetAsync(d0.b_counters.p, 0, sizeof(unsigned long long) * CT_N, d0.stream));
+            L.counters = (unsigned long long *)d0.b_counters.p;
+        }
+        hipEvent_t *ev = next_events(d0);
+        if ((r = rt_launch_frame(L, d0.stream, ev[0], ev[1])) != RT_OK) return r;
+        o = {L.rgb, L.hit_entity, L.hit_node, L.status};
+    } else {
+        if ((r = c->g_frame.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
+        o.rgb = (float *)c->g_frame.p;
+        if (ids) {
+            if ((r = c->g_hit_e.ensure(sizeof(int32_t) * P)) != RT_OK) return r;
+            if ((r = c->g_hit_n.ensure(sizeof(int32_t) * P)) != RT_OK) return r;
+            if ((r = c->g_status.ensure(P)) != RT_OK) return r;
+            o.hit_e = (int32_t *)c->g_hit_e.p;
+            o.hit_n = (int32_t *)c->g_hit_n.p;
+            o.status = (uint8_t *)c->g_status.p;
+        }
+        if (blend) HIP_TRY(hipMemcpyAsync(o.rgb, rgb_inout, sizeof(float) * 3 * P, hipMemcpyHostToDevice, d0.stream));
+        if ((r = frame_multi(c, cam, cfg, o, nullptr, stats != nullptr)) != RT_OK) return r;
+        HIP_TRY(hipSetDevice(d0.device));
     }
-    hipEvent_t *ev = c->ev[c->ev_next];
-    if ((r = rt_launch_frame(L, c->stream, ev[0], ev[1])) != RT_OK) return r;
-    HIP_TRY(hipMemcpyAsync(rgb_inout, L.rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost, c->stream));
-    if (hit_entity) HIP_TRY(hipMemcpyAsync(hit_entity, L.hit_entity, sizeof(int32_t) * P, hipMemcpyDeviceToHost, c->stream));
-    if (hit_node) HIP_TRY(hipMemcpyAsync(hit_node, L.hit_node, sizeof(int32_t) * P, hipMemcpyDeviceToHost, c->stream));
-    if (status) HIP_TRY(hipMemcpyAsync(status, L.status, P, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(rgb_inout, o.rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost, d0.stream));
+    if (hit_entity) HIP_TRY(hipMemcpyAsync(hit_entity, o.hit_e, sizeof(int32_t) * P, hipMemcpyDeviceToHost, d0.stream));
+    if (hit_node) HIP_TRY(hipMemcpyAsync(hit_node, o.hit_n, sizeof(int32_t) * P, hipMemcpyDeviceToHost, d0.stream));
+    if (status) HIP_TRY(hipMemcpyAsync(status, o.status, P, hipMemcpyDeviceToHost, d0.stream));
     int fault = 0;
-    HIP_TRY(hipMemcpyAsync(&fault, c->b_fault.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    unsigned long long h[CT_N] = {};
-    if (stats) HIP_TRY(hipMemcpyAsync(h, c->b_counters.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (stats) {
-        memset(stats, 0, sizeof *stats);
-        fill_stats(stats, h);
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
-        stats->kernel_ms = ms;
-        stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    }
+    if ((r = finish(c, 0, stats, t0, &fault)) != RT_OK) return r;
     if (fault) return rt_set_error(RT_E_FAULT, "a ray reached a state where the reference throws (status 2/3 pixels)");
     return RT_OK;
+}
+
+extern "C" int rt_trace_frame_device(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *d_rgb,
+                                     void *stream)
+{
+    int r = check_frame_args(c, cam, cfg);
+    if (r != RT_OK) return r;
+    if (!d_rgb) return rt_set_error(RT_E_INVALID, "rt_trace_frame_device: d_rgb is null");
+    DevGuard guard;
+    RtDevice &d0 = c->dev[0];
+    if ((r = use_device(d0)) != RT_OK) return r;
+    hipStream_t st = stream ? (hipStream_t)stream : d0.stream;
+    if (c->gather == RT_GATHER_NONE) {
+        RtLaunch L;
+        if ((r = prepare(c, d0, cam, cfg, 0, 1, cam->height, false, L)) != RT_OK) return r;
+        L.rgb = d_rgb;
+        HIP_TRY(hipMemsetAsync(d0.b_fault.p, 0, sizeof(int), st));
+        hipEvent_t *ev = next_events(d0);
+        return rt_launch_frame(L, st, ev[0], ev[1]);
+    }
+    const FrameOut o = {d_rgb, nullptr, nullptr, nullptr};
+    return frame_multi(c, cam, cfg, o, st, false);
+}
+
+extern "C" int rt_frame_fault(rt_ctx *c, int32_t *fault)
+{
+    if (!c || !fault) return rt_set_error(RT_E_INVALID, "rt_frame_fault: null argument");
+    DevGuard guard;
+    for (int k = 0; k < c->n_dev; k++) {          // the frame may have run on a caller's stream
+        HIP_TRY(hipSetDevice(c->dev[k].device));
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    int f = 0;
+    int r = finish(c, 0, nullptr, std::chrono::steady_clock::now(), &f);
+    *fault = f;
+    return r;
 }
 
 extern "C" int rt_trace_rows_device(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, int32_t part,
@@ -329,27 +681,30 @@ extern "C" int rt_trace_rows_device(rt_ctx *c, const rt_camera_desc *cam, const 
     const auto t0 = std::chrono::steady_clock::now();
     int r = check_frame_args(c, cam, cfg);
     if (r != RT_OK) return r;
+    if (c->n_dev != 1)
+        return rt_set_error(RT_E_INVALID, "rt_trace_rows_device: single-device contexts only (rt_trace_frame_device "
+                                          "splits a frame over a multi-device context)");
     if (n_parts < 1 || part < 0 || part >= n_parts || stripe_rows < 1)
         return rt_set_error(RT_E_INVALID, "rt_trace_rows_device: bad partition %d/%d stripe %d", part, n_parts, stripe_rows);
-    if ((r = use_device(c)) != RT_OK) return r;
+    DevGuard guard;
+    RtDevice &d0 = c->dev[0];
+    if ((r = use_device(d0)) != RT_OK) return r;
     RtLaunch L;
-    if ((r = prepare(c, cam, cfg, part, n_parts, stripe_rows, false, L)) != RT_OK) return r;
+    if ((r = prepare(c, d0, cam, cfg, part, n_parts, stripe_rows, false, L)) != RT_OK) return r;
     if (rows_out) *rows_out = L.rows;
     if (!d_rgb && L.rows > 0) return rt_set_error(RT_E_INVALID, "rt_trace_rows_device: d_rgb is null");
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = stream ? (hipStream_t)stream : d0.stream;
     L.rgb = (float *)d_rgb;
-    L.blend = cfg->col_weight != 1.0;
+    HIP_TRY(hipMemsetAsync(d0.b_fault.p, 0, sizeof(int), st));
     if (stats) {
-        HIP_TRY(hipMemsetAsync(c->b_counters.p, 0, sizeof(unsigned long long) * CT_N, st));
-        L.counters = (unsigned long long *)c->b_counters.p;
+        HIP_TRY(hipMemsetAsync(d0.b_counters.p, 0, sizeof(unsigned long long) * CT_N, st));
+        L.counters = (unsigned long long *)d0.b_counters.p;
     }
-    hipEvent_t *ev = c->ev[c->ev_next];
-    c->ev_next = (c->ev_next + 1) % rt_ctx::NEV;
-    c->ev_count = c->ev_count < rt_ctx::NEV ? c->ev_count + 1 : rt_ctx::NEV;
+    hipEvent_t *ev = next_events(d0);
     if ((r = rt_launch_frame(L, st, ev[0], ev[1])) != RT_OK) return r;
     if (stats) {
         unsigned long long h[CT_N] = {};
-        HIP_TRY(hipMemcpyAsync(h, c->b_counters.p, sizeof h, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(h, d0.b_counters.p, sizeof h, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         memset(stats, 0, sizeof *stats);
         fill_stats(stats, h);
@@ -367,13 +722,15 @@ extern "C" int rt_exposure_stats_device(rt_ctx *c, const float *d_rgb, int64_t n
 {
     if (!c || !out || n_pixels < 0 || (n_pixels > 0 && !d_rgb))
         return rt_set_error(RT_E_INVALID, "rt_exposure_stats_device: bad argument");
-    int r = use_device(c);
+    DevGuard guard;
+    RtDevice &d0 = c->dev[0];
+    int r = use_device(d0);
     if (r != RT_OK) return r;
     const int n_blocks = (int)(n_pixels / 256 + 1 < 1024 ? n_pixels / 256 + 1 : 1024);
     if ((r = c->b_stat.ensure(sizeof(double) * (2 * (size_t)n_blocks + 4))) != RT_OK) return r;
     double *d_out = (double *)c->b_stat.p;
     double *d_part = d_out + 4;
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = stream ? (hipStream_t)stream : d0.stream;
     if ((r = rt_launch_exposure_stats(d_rgb, (long long)n_pixels, d_part, n_blocks, d_out, st)) != RT_OK) return r;
     double h[3];
     HIP_TRY(hipMemcpyAsync(h, d_out, sizeof h, hipMemcpyDeviceToHost, st));
@@ -389,10 +746,12 @@ extern "C" int rt_tonemap_device(rt_ctx *c, const float *d_rgb, int64_t n_pixels
 {
     if (!c || n_pixels < 0 || (n_pixels > 0 && (!d_rgb || !d_rgba)))
         return rt_set_error(RT_E_INVALID, "rt_tonemap_device: bad argument");
-    int r = use_device(c);
+    DevGuard guard;
+    RtDevice &d0 = c->dev[0];
+    int r = use_device(d0);
     if (r != RT_OK) return r;
     return rt_launch_tonemap(d_rgb, (long long)n_pixels, drange_low, drange_high, d_rgba,
-                             stream ? (hipStream_t)stream : c->stream);
+                             stream ? (hipStream_t)stream : d0.stream);
 }
 
 // ToneMapper_DRLimited / _StdDevAroundMean / _AbsDevAroundMean / _Identity (src/view/tone_mapping.ts:22-80)
@@ -424,12 +783,17 @@ extern "C" int rt_tonemap_range(int32_t mode, const rt_exposure_stats *st, int32
 extern "C" int rt_kernel_times(rt_ctx *c, double *ms_out, int32_t n)
 {
     if (!c || (!ms_out && n > 0)) return rt_set_error(RT_E_INVALID, "rt_kernel_times: null argument");
-    int k = n < c->ev_count ? n : c->ev_count;
+    DevGuard guard;
+    RtDevice &d0 = c->dev[0];
+    int r = use_device(d0);
+    if (r != RT_OK) return r;
+    const int NEV = (int)d0.ev.size();
+    int k = n < d0.ev_count ? n : d0.ev_count;
     for (int i = 0; i < k; i++) {
-        const int idx = ((c->ev_next - k + i) % rt_ctx::NEV + rt_ctx::NEV) % rt_ctx::NEV;
-        HIP_TRY(hipEventSynchronize(c->ev[idx][1]));
+        const int idx = ((d0.ev_next - k + i) % NEV + NEV) % NEV;
+        HIP_TRY(hipEventSynchronize(d0.ev[idx][1]));
         float ms = 0;
-        HIP_TRY(hipEventElapsedTime(&ms, c->ev[idx][0], c->ev[idx][1]));
+        HIP_TRY(hipEventElapsedTime(&ms, d0.ev[idx][0], d0.ev[idx][1]));
         ms_out[i] = ms;
     }
     return k;
@@ -441,15 +805,17 @@ extern "C" int rt_debug_walk(rt_ctx *c, const double origin[3], const double dir
     if (!c || !origin || !dir || !out_tree || !out_octant || !n_out || max_out < 0)
         return rt_set_error(RT_E_INVALID, "rt_debug_walk: bad argument");
     if (!c->has_scene) return rt_set_error(RT_E_NOSCENE, "no scene uploaded");
+    DevGuard guard;
+    RtDevice &d0 = c->dev[0];
     int r;
-    if ((r = use_device(c)) != RT_OK) return r;
+    if ((r = use_device(d0)) != RT_OK) return r;
     if ((r = c->b_walk.ensure(sizeof(int32_t) * (2 * (size_t)max_out + 1))) != RT_OK) return r;
     int32_t *d_tree = (int32_t *)c->b_walk.p, *d_oct = d_tree + max_out, *d_n = d_oct + max_out;
-    if ((r = rt_launch_debug_walk(c->scene, origin, dir, include_undefined, max_out, d_tree, d_oct, d_n, c->stream)) != RT_OK)
+    if ((r = rt_launch_debug_walk(d0.scene, origin, dir, include_undefined, max_out, d_tree, d_oct, d_n, d0.stream)) != RT_OK)
         return r;
     int32_t n = 0;
-    HIP_TRY(hipMemcpyAsync(&n, d_n, sizeof n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpyAsync(&n, d_n, sizeof n, hipMemcpyDeviceToHost, d0.stream));
+    HIP_TRY(hipStreamSynchronize(d0.stream));
     if (n < 0) return rt_set_error(RT_E_FAULT, "rt_debug_walk: the walker threw");
     HIP_TRY(hipMemcpy(out_tree, d_tree, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(out_octant, d_oct, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
@@ -462,23 +828,25 @@ extern "C" int rt_debug_camera_dirs(rt_ctx *c, const rt_camera_desc *cam, double
     if (!c || !cam || !dirs_out) return rt_set_error(RT_E_INVALID, "rt_debug_camera_dirs: null argument");
     if (!c->has_scene) return rt_set_error(RT_E_NOSCENE, "no scene uploaded");
     if (cam->width <= 0 || cam->height <= 0) return rt_set_error(RT_E_INVALID, "bad screen size");
+    DevGuard guard;
+    RtDevice &d0 = c->dev[0];
     int r;
-    if ((r = use_device(c)) != RT_OK) return r;
+    if ((r = use_device(d0)) != RT_OK) return r;
     rt_config_desc cfg;
     memset(&cfg, 0, sizeof cfg);
     cfg.refmax = 1;
     cfg.default_substance = -1;
     cfg.col_weight = 1;
     RtLaunch L;
-    if ((r = prepare(c, cam, &cfg, 0, 1, cam->height, false, L)) != RT_OK) return r;
+    if ((r = prepare(c, d0, cam, &cfg, 0, 1, cam->height, false, L)) != RT_OK) return r;
     const size_t P = (size_t)cam->width * (size_t)cam->height;
-    if ((r = c->b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
-    L.rgb = (float *)c->b_rgb.p;
+    if ((r = d0.b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
+    L.rgb = (float *)d0.b_rgb.p;
     L.skip_trace = 1;
-    if ((r = rt_launch_frame(L, c->stream, nullptr, nullptr)) != RT_OK) return r;
+    if ((r = rt_launch_frame(L, d0.stream, nullptr, nullptr)) != RT_OK) return r;
     std::vector<double> soa(3 * P);
-    HIP_TRY(hipMemcpyAsync(soa.data(), L.dirs, sizeof(double) * 3 * P, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpyAsync(soa.data(), L.dirs, sizeof(double) * 3 * P, hipMemcpyDeviceToHost, d0.stream));
+    HIP_TRY(hipStreamSynchronize(d0.stream));
     for (size_t p = 0; p < P; p++)
         for (int i = 0; i < 3; i++) {
             const size_t x = p % (size_t)cam->width, y = p / (size_t)cam->width;

@@ -103,10 +103,12 @@ enum { CT_SEG, CT_RET, CT_SLOT, CT_LOC, CT_SPH, CT_BOX, CT_TRI, CT_HIT, CT_PRIM,
 
 // The resident scene (rt_scene.hip): full upload or incremental update into stable device slots.
 struct RtSceneStore;
-RtSceneStore *rt_store_new(bool sah);
+// The store replicates the scene on `ndev` devices (one stream each); rt_store_upload fills dev[k]
+// for every device k.
+RtSceneStore *rt_store_new(bool sah, int ndev, const int *devs, void *const *streams);
 void rt_store_free(RtSceneStore *st);
-int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, void *stream, RtDevScene *dev,
-                    bool *scatter, rt_update_stats *stats);
+int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, RtDevScene *dev, bool *scatter,
+                    rt_update_stats *stats);
 
 // Kernel launchers (rt_kernels.hip).
 struct RtLaunch {
@@ -153,6 +155,29 @@ int rt_launch_exposure_stats(const float *d_rgb, long long n, double *d_partials
 int rt_launch_tonemap(const float *d_rgb, long long n, double low, double high, uint8_t *d_rgba, void *stream);
 int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[3], int include_undefined,
                          int max_out, int32_t *d_tree, int32_t *d_oct, int32_t *d_n, void *stream);
+
+// ---- multi-device frame assembly (rt_multi.hip) -------------------------------------------------------
+// Rows between a frame (H rows of row_bytes) and the stacked parts (n_parts x max_rows rows):
+// to_frame = 1 de-interleaves the gathered parts into the frame, 0 deals the frame out.
+int rt_launch_stripes(const void *src, void *dst, int H, int n_parts, int stripe, int max_rows, size_t row_bytes,
+                      int to_frame, void *stream);
+
+// RCCL entry points (rccl/rccl.h), resolved by rt_rccl() with dlopen on first use.  Declared with
+// plain types so this header stays host-compiler clean: ncclResult_t / ncclDataType_t are int
+// enums, ncclComm_t and hipStream_t pointers (rt_multi.hip checks the constants against rccl.h).
+enum { RT_NCCL_UINT8 = 1, RT_NCCL_INT32 = 2, RT_NCCL_FLOAT32 = 7 };
+struct RtRccl {
+    bool ok;
+    int (*comm_init_all)(void **comms, int ndev, const int *devlist);
+    int (*comm_destroy)(void *comm);
+    int (*gather)(const void *send, void *recv, size_t count, int dtype, int root, void *comm, void *stream);
+    int (*scatter)(const void *send, void *recv, size_t count, int dtype, int root, void *comm, void *stream);
+    int (*group_start)(void);
+    int (*group_end)(void);
+    const char *(*error_string)(int);
+};
+const RtRccl *rt_rccl(void);        // null when librccl is unavailable (rt_rccl_error() says why)
+const char *rt_rccl_error(void);
 
 // Row bookkeeping for the stripe partition.
 static inline int32_t rt_part_rows(int32_t H, int32_t part, int32_t n_parts, int32_t stripe)

@@ -14,6 +14,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <utility>
+#include <vector>
 
 #include "rt_internal.h"
 #include "rt_jsnum.h"
@@ -24,7 +28,7 @@ namespace {
 
 constexpr int ST_OK = 0, ST_WARN = 1, ST_FAULT = 2, ST_CAP = 3;
 constexpr int ST_DEFER = 100;                    // split path: continuation queued, pixel written later
-constexpr long long STEP_CAP = 1ll << 24;        // per-ray loop bound: every lane terminates
+constexpr int STEP_CAP = 1 << 24;                // per-walk loop bound: every lane terminates
 
 // ---- node access --------------------------------------------------------------------------------
 struct NodeDims { double x, y, z, s; };
@@ -118,6 +122,7 @@ struct Walker {
     int cur_oct;           // RT_OCT_UNDEF, 0..7, or RT_OCT_BAD
     int depth;
     int flags;
+    int steps;             // loop iterations of this walk (bounded by STEP_CAP)
 };
 
 struct Counters {
@@ -132,6 +137,7 @@ __device__ int walker_setup(const RtDevScene &S, Walker &w)
     w.nn = 0;
     w.flags = 0;
     w.depth = 0;
+    w.steps = 0;                                             // STEP_CAP counts per walk
     if (w.cur_tree >= 0) return 1;
     const NodeDims r = node_dims(S, 0);
     BoxIsect bi;
@@ -286,7 +292,7 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
                            int stop = -1)
 {
     while (w.cur_tree >= 0) {
-        if (++c.steps > STEP_CAP) return -2;
+        if (++w.steps > STEP_CAP) return -2;
         const int ltree = w.cur_tree, loct = w.cur_oct;
         int lnode;
         if (loct != RT_OCT_UNDEF) {
@@ -1042,7 +1048,7 @@ __device__ __forceinline__ int cont_g(const RtLaunch &L)
     const int n = *lvl_ctr(L, L.level - 1);
     int g = L.cont_group;
     while (g < 64 && (long long)g * 4096 < (long long)n) g *= 2;
-    return g;
+    return g < 64 ? g : 64;                       // a wave holds 64 lanes, whatever RT_CONT_GROUP was
 }
 
 __device__ __forceinline__ int n_items(const RtLaunch &L)
@@ -1497,21 +1503,33 @@ __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, doub
     } while (0)
 
 // Persistent grid: every CU filled to the occupancy the kernel's registers admit.  The tile queue
-// makes an over-estimate harmless (late blocks find the queue empty).
+// makes an over-estimate harmless (late blocks find the queue empty).  The CU count and each
+// kernel's blocks per CU are queried once (all devices of a context are MI355X): one host thread
+// issues the launches of up to 8 GPUs, so a launch is only the launch.
 static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const RtLaunch &L)
 {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus < 1) cus = 1;
+    static std::atomic<int> cus{0};
+    static std::mutex mu;
+    static std::vector<std::pair<const void *, int>> per_kernel;
+    const void *kp = reinterpret_cast<const void *>(kernel);
+    int n_cu = cus.load(std::memory_order_relaxed), per = 0;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!n_cu) {
+            int dev = 0, v = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+            n_cu = v < 1 ? 1 : v;
+            cus.store(n_cu);
+        }
+        for (const auto &e : per_kernel)
+            if (e.first == kp) per = e.second;
+        if (!per) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kp, 256, 0) != hipSuccess || per < 1) per = 1;
+            per_kernel.emplace_back(kp, per);
+        }
     }
-    int per = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void *>(kernel), 256, 0) != hipSuccess ||
-        per < 1)
-        per = 1;
-    hipLaunchKernelGGL(kernel, dim3(cus * per), dim3(256), 0, st, L);
+    hipLaunchKernelGGL(kernel, dim3(n_cu * per), dim3(256), 0, st, L);
 }
 
 int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end)
@@ -1519,11 +1537,15 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     hipStream_t st = (hipStream_t)stream;
     const int W = L.cam.width;
     const int rg_lanes = 6 * (L.rows > 0 ? L.rows : 0);
+    (void)hipGetLastError();                     // a stale error of an earlier runtime call is not ours
     hipLaunchKernelGGL(k_frame_start, dim3(1 + (rg_lanes + 255) / 256), dim3(256), 0, st, L.scene, L.cam, L.cfg,
                        L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.dirs);
     HIP_TRY(hipGetLastError());
-    if (L.rows <= 0) return RT_OK;
-    if (L.skip_trace) return RT_OK;
+    if (L.rows <= 0 || L.skip_trace) {           // an empty part (more devices than stripes): no trace
+        if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
+        if (ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
+        return RT_OK;
+    }
     (void)W;
     HIP_TRY(hipMemsetAsync(L.ctr, 0, sizeof(int32_t) * RT_CTR_INTS, st));
     if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));

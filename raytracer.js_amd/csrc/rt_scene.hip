@@ -255,20 +255,37 @@ struct RtSceneStore {
     std::vector<RtImage> m_images;
     std::vector<uint8_t> m_texels;                     // all images' bytes, padded to 4
     size_t list_used = 0, bvh_used = 0;
-    DevArr a[A_N];
+    // the scene is replicated on every device of the context: one set of host mirrors, one set of
+    // device arrays (and one staging buffer) per device, all written from the same staging bytes
+    int ndev = 1;
+    int devs[RT_MAX_DEVICES] = {};
+    hipStream_t sts[RT_MAX_DEVICES] = {};
+    DevArr a[RT_MAX_DEVICES][A_N];
     // staging
     uint8_t *pinned = nullptr;
     size_t pinned_cap = 0;
-    DevArr dstage;
+    DevArr dstage[RT_MAX_DEVICES];
     std::vector<uint8_t> stage;
     struct Pending { int arr; size_t off, bytes, src; };
     std::vector<Pending> pend;
 
     ~RtSceneStore()
     {
-        for (DevArr &d : a) d.release();
-        dstage.release();
+        for (int k = 0; k < ndev; k++) {
+            (void)hipSetDevice(devs[k]);
+            for (DevArr &d : a[k]) d.release();
+            dstage[k].release();
+        }
         if (pinned) (void)hipHostFree(pinned);
+    }
+
+    int sync_all()
+    {
+        for (int k = 0; k < ndev; k++) {
+            HIP_TRY(hipSetDevice(devs[k]));
+            HIP_TRY(hipStreamSynchronize(sts[k]));
+        }
+        return RT_OK;
     }
 
     void add(int arr, size_t off, const void *src, size_t bytes)
@@ -310,35 +327,47 @@ struct RtSceneStore {
         }
     }
 
-    int flush(hipStream_t st, int64_t *bytes_out)
+    int flush(int64_t *bytes_out)
     {
         const size_t nch = pend.size();
         if (!nch) return RT_OK;
-        const size_t tab = (stage.size() + 15) & ~(size_t)15, total = tab + nch * sizeof(Chunk);
-        if (total > pinned_cap) {
-            const size_t nc = std::max<size_t>(std::max(total, 2 * pinned_cap), 8u << 20);   // hipHostMalloc is slow
+        // pinned: [staged bytes | chunk table of device 0 | ... of device ndev-1]; each device gets
+        // the staged bytes and its own table (the destination addresses differ), so all devices'
+        // copies and scatter kernels run concurrently
+        const size_t tab = (stage.size() + 15) & ~(size_t)15, tsz = nch * sizeof(Chunk), total = tab + tsz;
+        const size_t need = tab + (size_t)ndev * tsz;
+        if (need > pinned_cap) {
+            const size_t nc = std::max<size_t>(std::max(need, 2 * pinned_cap), 8u << 20);   // hipHostMalloc is slow
             if (pinned) (void)hipHostFree(pinned);
             pinned = nullptr;
             pinned_cap = 0;
             HIP_TRY(hipHostMalloc((void **)&pinned, nc, hipHostMallocDefault));
             pinned_cap = nc;
         }
-        int r = dstage.reserve(total, 0, st);
-        if (r != RT_OK) return r;
         memcpy(pinned, stage.data(), stage.size());
-        Chunk *tabp = reinterpret_cast<Chunk *>(pinned + tab);
-        for (size_t k = 0; k < nch; k++)
-            tabp[k] = {(uint64_t)(uintptr_t)a[pend[k].arr].p + pend[k].off, pend[k].src, pend[k].bytes};
-        HIP_TRY(hipMemcpyAsync(dstage.p, pinned, total, hipMemcpyHostToDevice, st));
-        const uint8_t *dev = (const uint8_t *)dstage.p;
-        for (size_t k0 = 0; k0 < nch; k0 += 65535) {
-            const unsigned nb = (unsigned)std::min<size_t>(65535, nch - k0);
-            hipLaunchKernelGGL(k_scene_patch, dim3(nb), dim3(256), 0, st,
-                               reinterpret_cast<const Chunk *>(dev + tab) + k0, dev);
-            HIP_TRY(hipGetLastError());
+        for (int d = 0; d < ndev; d++) {
+            Chunk *tabp = reinterpret_cast<Chunk *>(pinned + tab + (size_t)d * tsz);
+            for (size_t k = 0; k < nch; k++)
+                tabp[k] = {(uint64_t)(uintptr_t)a[d][pend[k].arr].p + pend[k].off, pend[k].src, pend[k].bytes};
         }
-        HIP_TRY(hipStreamSynchronize(st));
-        *bytes_out += (int64_t)total;
+        for (int d = 0; d < ndev; d++) {
+            HIP_TRY(hipSetDevice(devs[d]));
+            const hipStream_t sd = sts[d];
+            int r = dstage[d].reserve(total, 0, sd);
+            if (r != RT_OK) return r;
+            uint8_t *dev = (uint8_t *)dstage[d].p;
+            HIP_TRY(hipMemcpyAsync(dev, pinned, tab, hipMemcpyHostToDevice, sd));
+            HIP_TRY(hipMemcpyAsync(dev + tab, pinned + tab + (size_t)d * tsz, tsz, hipMemcpyHostToDevice, sd));
+            for (size_t k0 = 0; k0 < nch; k0 += 65535) {
+                const unsigned nb = (unsigned)std::min<size_t>(65535, nch - k0);
+                hipLaunchKernelGGL(k_scene_patch, dim3(nb), dim3(256), 0, sd,
+                                   reinterpret_cast<const Chunk *>(dev + tab) + k0, dev);
+                HIP_TRY(hipGetLastError());
+            }
+            *bytes_out += (int64_t)total;
+        }
+        int r = sync_all();
+        if (r != RT_OK) return r;
         stage.clear();
         pend.clear();
         return RT_OK;
@@ -361,21 +390,25 @@ struct RtSceneStore {
 
     // Device capacities for the current high-water marks, keeping what is resident.
     int reserve_all(size_t n_slots, size_t n_ent, size_t n_shades, size_t n_ri, size_t n_img, size_t n_tex,
-                    hipStream_t st, bool keep)
+                    bool keep)
     {
         const size_t need[A_N] = {sizeof(RtNode) * n_slots, 8 * n_slots, 16 * n_slots, 4 * n_slots,
                                   sizeof(RtPrim) * list_used, sizeof(RtBvh) * bvh_used, 4 * list_used,
                                   16 * list_used, sizeof(rt_shade) * n_shades, 4 * n_ent, 8 * n_ri,
                                   sizeof(RtImage) * n_img, n_tex};
-        for (int k = 0; k < A_N; k++) {
-            int r = a[k].reserve(need[k], keep ? a[k].cap : 0, st);
-            if (r != RT_OK) return r;
+        for (int d = 0; d < ndev; d++) {
+            HIP_TRY(hipSetDevice(devs[d]));
+            for (int k = 0; k < A_N; k++) {
+                int r = a[d][k].reserve(need[k], keep ? a[d][k].cap : 0, sts[d]);
+                if (r != RT_OK) return r;
+            }
         }
         return RT_OK;
     }
 
-    void fill(const rt_scene_desc *s, RtDevScene &d) const
+    void fill(const rt_scene_desc *s, int k, RtDevScene &d) const
     {
+        const DevArr *a = this->a[k];
         d.node = (const RtNode *)a[A_NODE].p;
         d.node_up = (const int32_t *)a[A_NODE_UP].p;
         d.node_ent = (const int32_t *)a[A_NODE_ENT].p;
@@ -410,7 +443,7 @@ struct RtSceneStore {
     }
 
     // Full upload: slots in DFS order, regions packed exactly.
-    int full(const rt_scene_desc *s, const std::vector<int32_t> &oct, hipStream_t st, rt_update_stats &us)
+    int full(const rt_scene_desc *s, const std::vector<int32_t> &oct, rt_update_stats &us)
     {
         const int N = s->n_nodes, NL = s->n_list;
         const auto t0 = std::chrono::steady_clock::now();
@@ -471,8 +504,7 @@ struct RtSceneStore {
         entity_mirrors(s);
         us.host_ms = ms_since(t0);
         pack_images(s, m_images, m_texels);
-        int r = reserve_all(N, s->n_entities, s->n_shades, s->n_substances, m_images.size(), m_texels.size(), st,
-                            false);
+        int r = reserve_all(N, s->n_entities, s->n_shades, s->n_substances, m_images.size(), m_texels.size(), false);
         if (r != RT_OK) return r;
         const void *src[A_N] = {m_node.data(), m_up.data(), m_ent.data(), m_dfs.data(), prim.data(),
                                 bvh.data(), m_list.data(), prefix.data(), s->shades, s->ent_substance, s->substance_ri,
@@ -481,12 +513,15 @@ struct RtSceneStore {
                                    sizeof(RtPrim) * lb, sizeof(RtBvh) * bb, 4 * lb, 16 * lb,
                                    sizeof(rt_shade) * (size_t)s->n_shades, 4 * (size_t)s->n_entities,
                                    8 * (size_t)s->n_substances, sizeof(RtImage) * m_images.size(), m_texels.size()};
-        for (int k = 0; k < A_N; k++) {
-            if (!bytes[k]) continue;
-            HIP_TRY(hipMemcpyAsync(a[k].p, src[k], bytes[k], hipMemcpyHostToDevice, st));
-            us.bytes += (int64_t)bytes[k];
+        for (int d = 0; d < ndev; d++) {
+            HIP_TRY(hipSetDevice(devs[d]));
+            for (int k = 0; k < A_N; k++) {
+                if (!bytes[k]) continue;
+                HIP_TRY(hipMemcpyAsync(a[d][k].p, src[k], bytes[k], hipMemcpyHostToDevice, sts[d]));
+                us.bytes += (int64_t)bytes[k];
+            }
         }
-        HIP_TRY(hipStreamSynchronize(st));
+        if ((r = sync_all()) != RT_OK) return r;
         us.full = 1;
         us.dirty_nodes = N;
         us.changed_entities = s->n_entities;
@@ -495,7 +530,7 @@ struct RtSceneStore {
     }
 
     // Incremental update; returns 1 when the scene is not an edit of the resident one (caller does full).
-    int update(const rt_scene_desc *s, const std::vector<int32_t> &oct, hipStream_t st, rt_update_stats &us)
+    int update(const rt_scene_desc *s, const std::vector<int32_t> &oct, rt_update_stats &us)
     {
         const int N = s->n_nodes, NL = s->n_list, NE = s->n_entities;
         const auto t0 = std::chrono::steady_clock::now();
@@ -581,7 +616,7 @@ struct RtSceneStore {
         std::vector<uint8_t> n_texels;
         pack_images(s, n_images, n_texels);
         int r = reserve_all(n_slots, NE, s->n_shades, s->n_substances, n_images.size(),
-                            std::max(n_texels.size(), m_texels.size()), st, true);
+                            std::max(n_texels.size(), m_texels.size()), true);
         if (r != RT_OK) return r;
         m_list.resize(lu, -1);
         m_node.resize(n_slots);                       // new slots start zeroed
@@ -689,7 +724,7 @@ struct RtSceneStore {
         m_shade.assign(s->ent_shade, s->ent_shade + NE);
         m_geom.assign(s->ent_geom, s->ent_geom + 9 * (size_t)NE);
         us.host_ms += ms_since(t0);
-        if ((r = flush(st, &us.bytes)) != RT_OK) {
+        if ((r = flush(&us.bytes)) != RT_OK) {
             has = false;                            // the device copy is no longer known
             return r;
         }
@@ -702,17 +737,24 @@ struct RtSceneStore {
     }
 };
 
-RtSceneStore *rt_store_new(bool sah)
+RtSceneStore *rt_store_new(bool sah, int ndev, const int *devs, void *const *streams)
 {
+    if (ndev < 1 || ndev > RT_MAX_DEVICES) return nullptr;
     RtSceneStore *st = new (std::nothrow) RtSceneStore();
-    if (st) st->sah = sah;
+    if (!st) return nullptr;
+    st->sah = sah;
+    st->ndev = ndev;
+    for (int k = 0; k < ndev; k++) {
+        st->devs[k] = devs[k];
+        st->sts[k] = (hipStream_t)streams[k];
+    }
     return st;
 }
 
 void rt_store_free(RtSceneStore *st) { delete st; }
 
-int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, void *stream, RtDevScene *dev,
-                    bool *scatter, rt_update_stats *stats)
+int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, RtDevScene *dev, bool *scatter,
+                    rt_update_stats *stats)
 {
     const auto t0 = std::chrono::steady_clock::now();
     rt_update_stats us;
@@ -722,20 +764,22 @@ int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, 
     int r = validate(s, oct, sc);
     if (r != RT_OK) return r;
     const double validate_ms = ms_since(t0);
-    hipStream_t hs = (hipStream_t)stream;
     r = 1;
     if (incremental) {
-        HIP_TRY(hipDeviceSynchronize());            // no frame may read the scene while it changes
-        r = st->update(s, oct, hs, us);
+        for (int k = 0; k < st->ndev; k++) {        // no frame may read the scene while it changes
+            HIP_TRY(hipSetDevice(st->devs[k]));
+            HIP_TRY(hipDeviceSynchronize());
+        }
+        r = st->update(s, oct, us);
         if (r < 0) return r;
     }
     if (r == 1) {
         memset(&us, 0, sizeof us);
-        r = st->full(s, oct, hs, us);
+        r = st->full(s, oct, us);
         if (r != RT_OK) return r;
     }
     us.host_ms += validate_ms;
-    st->fill(s, *dev);
+    for (int k = 0; k < st->ndev; k++) st->fill(s, k, dev[k]);
     *scatter = sc;
     us.total_ms = ms_since(t0);
     if (stats) *stats = us;

@@ -143,14 +143,37 @@ void finalize_ctx(napi_env, void *data, void *)
     delete slot;
 }
 
+// create(device) or create([devices...], stripe_rows): rt_create_desc (include/rt.h).  A list
+// makes one context drive several GPUs: row stripes per device, gathered on devices[0] over RCCL.
 napi_value Create(napi_env env, napi_callback_info info)
 {
-    size_t argc = 1;
-    napi_value argv[1];
+    size_t argc = 2;
+    napi_value argv[2];
     NAPI_TRY(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
-    int32_t dev = 0;
-    if (argc >= 1) napi_get_value_int32(env, argv[0], &dev);
-    rt_create_desc d = {dev, 0};
+    rt_create_desc d;
+    memset(&d, 0, sizeof d);
+    bool is_list = false;
+    if (argc >= 1) NAPI_TRY(napi_is_array(env, argv[0], &is_list));
+    if (is_list) {
+        uint32_t n = 0;
+        NAPI_TRY(napi_get_array_length(env, argv[0], &n));
+        if (n < 1 || n > RT_MAX_DEVICES) {
+            napi_throw_error(env, "RT_E_INVALID", "devices: a list of 1..8 GPU ordinals");
+            return nullptr;
+        }
+        d.n_devices = (int32_t)n;
+        for (uint32_t k = 0; k < n; k++) {
+            napi_value v;
+            NAPI_TRY(napi_get_element(env, argv[0], k, &v));
+            if (napi_get_value_int32(env, v, &d.devices[k]) != napi_ok) {
+                napi_throw_error(env, "RT_E_INVALID", "devices: a list of 1..8 GPU ordinals");
+                return nullptr;
+            }
+        }
+    } else if (argc >= 1) {
+        napi_get_value_int32(env, argv[0], &d.device);
+    }
+    if (argc >= 2) napi_get_value_int32(env, argv[1], &d.stripe_rows);
     rt_ctx *ctx = nullptr;
     if (throw_rc(env, rt_create(&d, &ctx))) return nullptr;
     rt_ctx **slot = new rt_ctx *(ctx);

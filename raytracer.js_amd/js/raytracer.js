@@ -252,7 +252,10 @@ function camera_desc(camera) {
 /* ---- the drop-in ------------------------------------------------------------------------------- */
 
 class Raytracer {
-	/** Same signature as the reference (src/raytracer.ts:291-298); `options.device` picks the GPU.
+	/** Same signature as the reference (src/raytracer.ts:291-298); `options.device` picks the GPU, or
+	 * `options.devices` (e.g. [0,1,2,3,4,5,6,7]) splits every frame over several GPUs of the node:
+	 * 8-row stripes dealt round-robin (`options.stripe_rows`), each GPU holding a replica of the
+	 * scene, the parts gathered on devices[0] over RCCL and copied into the ebuffer once.
 	 * `options.scatter === 'counter'` renders rough mirrors with the counter-based RNG (include/rt.h
 	 * RT_SCATTER_COUNTER), keyed each frame by one draw of this Raytracer's rng; otherwise they are
 	 * rejected (RT_E_UNSUPPORTED), as scatter_ray's sequential PRNG cannot be reproduced in parallel. */
@@ -288,7 +291,11 @@ class Raytracer {
 
 	_sync_scene() {
 		const a = load_addon();
-		if (!this._ctx) this._ctx = a.create(this.options.device | 0);
+		if (!this._ctx) {
+			const o = this.options;
+			this._ctx = Array.isArray(o.devices) ? a.create(o.devices.map((x) => x | 0), (o.stripe_rows | 0))
+				: a.create(o.device | 0);
+		}
 		const sky = this.config.sky.texture;
 		if (this._scene && loaded_image(sky) && !this._scene._maps.image_index.has(sky)) this._dirty = true;
 		if (!this._scene) {

@@ -191,15 +191,43 @@ def build_scene(spec):
 
 
 class Context:
-    """One rt_ctx bound to one GPU."""
+    """One rt_ctx: one GPU (`device`), or a list of GPUs (`devices`) over which every frame is split
+    into row stripes of `stripe_rows` and gathered on devices[0] (RCCL, or device copies when a
+    device is listed twice or flags has RT_CREATE_PEER_GATHER)."""
 
-    def __init__(self, device=0, flags=0):
+    def __init__(self, device=0, flags=0, devices=None, stripe_rows=0):
         self.L = load_library()
-        cd = abi.rt_create_desc(device=int(device), flags=int(flags))
+        cd = abi.rt_create_desc(device=int(device), flags=int(flags), stripe_rows=int(stripe_rows))
+        if devices is not None:
+            devices = [int(d) for d in devices]
+            if not 1 <= len(devices) <= abi.RT_MAX_DEVICES:
+                raise ValueError("1..%d devices, got %r" % (abi.RT_MAX_DEVICES, devices))
+            cd.n_devices = len(devices)
+            for k, d in enumerate(devices):
+                cd.devices[k] = d
         h = C.c_void_p()
         _check(self.L.rt_create(C.byref(cd), C.byref(h)))
         self.h = h
         self.scene = None
+
+    def info(self):
+        """rt_ctx_info: {n_devices, devices, stripe_rows, gather ('none' | 'rccl' | 'peer')}."""
+        i = abi.rt_ctx_info()
+        _check(self.L.rt_ctx_info_get(self.h, C.byref(i)))
+        return dict(n_devices=i.n_devices, devices=list(i.devices[:i.n_devices]), stripe_rows=i.stripe_rows,
+                    gather={abi.RT_GATHER_NONE: "none", abi.RT_GATHER_RCCL: "rccl",
+                            abi.RT_GATHER_PEER: "peer"}[i.gather])
+
+    def trace_frame_device(self, cam, cfg, d_rgb_ptr, stream_ptr=None):
+        """rt_trace_frame_device: the whole frame into a devices[0] buffer (W*H*3 f32), asynchronous."""
+        _check(self.L.rt_trace_frame_device(self.h, C.byref(cam), C.byref(cfg), C.c_void_p(d_rgb_ptr),
+                                            C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def frame_fault(self):
+        """rt_frame_fault: synchronises; True when a ray of the last issued frame hit a reference throw."""
+        f = C.c_int32()
+        _check(self.L.rt_frame_fault(self.h, C.byref(f)))
+        return bool(f.value)
 
     def close(self):
         if self.h:

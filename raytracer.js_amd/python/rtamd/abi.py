@@ -22,6 +22,9 @@ RT_RESP_REFLECTION, RT_RESP_TRANSMISSION, RT_RESP_BOTH = 0, 1, 2
 STATUS_OK, STATUS_WARN, STATUS_FAULT, STATUS_CAP = 0, 1, 2, 3
 RT_CREATE_NO_CULL = 1
 RT_CREATE_NO_SPLIT = 2
+RT_CREATE_PEER_GATHER = 4
+RT_MAX_DEVICES = 8
+RT_GATHER_NONE, RT_GATHER_RCCL, RT_GATHER_PEER = 0, 1, 2
 
 _d = C.c_double
 _i = C.c_int32
@@ -102,7 +105,12 @@ class rt_update_stats(C.Structure):
 
 
 class rt_create_desc(C.Structure):
-    _fields_ = [("device", _i), ("flags", _i)]
+    _fields_ = [("device", _i), ("flags", _i), ("n_devices", _i), ("stripe_rows", _i),
+                ("devices", _i * RT_MAX_DEVICES)]
+
+
+class rt_ctx_info(C.Structure):
+    _fields_ = [("n_devices", _i), ("devices", _i * RT_MAX_DEVICES), ("stripe_rows", _i), ("gather", _i)]
 
 
 class rt_entity_in(C.Structure):
@@ -120,7 +128,8 @@ EXPORTS = ("rt_create", "rt_destroy", "rt_last_error", "rt_abi_version", "rt_upl
            "rt_trace_frame", "rt_trace_rows_device", "rt_kernel_times", "rt_debug_walk",
            "rt_debug_camera_dirs", "rt_builder_create", "rt_builder_destroy", "rt_builder_add",
            "rt_builder_add_many", "rt_builder_desc", "rt_exposure_stats_device", "rt_tonemap_device",
-           "rt_tonemap_range", "rt_update_scene", "rt_builder_move", "rt_builder_set_shade")
+           "rt_tonemap_range", "rt_update_scene", "rt_builder_move", "rt_builder_set_shade",
+           "rt_trace_frame_device", "rt_frame_fault", "rt_ctx_info_get")
 
 
 def declare(lib):
@@ -152,6 +161,9 @@ def declare(lib):
     lib.rt_update_scene.argtypes = [vp, P(rt_scene_desc), P(rt_update_stats)]
     lib.rt_builder_move.argtypes = [vp, _i, _pd]
     lib.rt_builder_set_shade.argtypes = [vp, _i, _i, _i]
+    lib.rt_trace_frame_device.argtypes = [vp, P(rt_camera_desc), P(rt_config_desc), vp, vp]
+    lib.rt_frame_fault.argtypes = [vp, _pi]
+    lib.rt_ctx_info_get.argtypes = [vp, P(rt_ctx_info)]
     return lib
 
 

@@ -1,5 +1,6 @@
 /*
  * run_dropin.js <scene.json> <out_prefix> [--serialize-only] [--scatter <seed>] [--edit A B C]
+ *               [--devices 0,0,0]
  * Builds reference-shaped objects, checks serialize_scene() reproduces the linearised arrays, and
  * (unless --serialize-only) renders one frame with the drop-in Raytracer into ExposureBuffer.pixels.
  * --scatter: rough mirrors with options.scatter = 'counter', the rng's one draw = seed / 2^53.
@@ -8,6 +9,7 @@
  *   sphere A is moved to (0.5, 0.5, 0.8) (Entity._set_pos + Set.delete / Set.add into the root's
  *   EntitySet, which is where add_entity_to_octree files a cube straddling the centre planes), and
  *   entity B takes entity C's material and texture (set_material / set_texture).
+ * --devices: options.devices (one context over several GPUs, or several parts on one GPU).
  */
 'use strict';
 const fs = require('fs');
@@ -53,8 +55,10 @@ const config = {
 const si = process.argv.indexOf('--scatter');
 const seed = si > 0 ? Number(process.argv[si + 1]) : null;
 const rng = seed === null ? null : { next: () => seed / 9007199254740992 };
-const tracer = new rt.Raytracer(config, world.root, cam, eb, rng,
-	seed === null ? { keep_ids: true } : { keep_ids: true, scatter: 'counter' });
+const di = process.argv.indexOf('--devices');
+const opts = seed === null ? { keep_ids: true } : { keep_ids: true, scatter: 'counter' };
+if (di > 0) opts.devices = process.argv[di + 1].split(',').map(Number);
+const tracer = new rt.Raytracer(config, world.root, cam, eb, rng, opts);
 const t0 = process.hrtime.bigint();
 tracer.trace_frame();
 const t1 = process.hrtime.bigint();

@@ -1,0 +1,66 @@
+"""bench.py's launcher logic and roofline arithmetic, on CPU (no GPU calls).
+
+`--gpus N` must either run N GPUs or fail loudly: under torchrun WORLD_SIZE must equal N; without
+torchrun N > 1 runs one process over N GPUs and exits 2 when the host has fewer."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _bench(args, env_extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=300)
+
+
+def test_world_size_must_match_gpus():
+    r = _bench(["--gpus", "2", "--steps", "1"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2, r.stderr
+    assert "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_more_gpus_than_the_host_has_fails():
+    import torch
+    n = torch.cuda.device_count()
+    r = _bench(["--gpus", str(n + 1), "--steps", "1"], {})
+    assert r.returncode == 2, r.stderr
+    assert "needs %d GPUs, this host has %d" % (n + 1, n) in r.stderr
+
+
+def test_kernel_names_and_rooflines():
+    import bench
+    assert bench._kernel_base("(anonymous namespace)::k_walk<4>(RtLaunch)") == "k_walk"
+    assert bench._kernel_base("void (anonymous namespace)::k_walk_seg<2>(RtLaunch)") == "k_walk_seg"
+    assert bench._kernel_base("k_first_seg<4>") == "k_first_seg"
+    dur = {"k_walk": 2.0, "k_walk_seg": 0.5, "k_first": 1.0}
+    pmc = {"k_walk": dict(FETCH_SIZE=1000.0, WRITE_SIZE=500.0, SQ_INSTS_VALU=1e9, SQ_INSTS_VALU_ADD_F64=1e8,
+                          SQ_INSTS_VALU_MUL_F64=1e8, SQ_INSTS_VALU_FMA_F64=0.0, SQ_INSTS_VALU_TRANS_F64=0.0,
+                          GRBM_GUI_ACTIVE=8 * 2.0e9 * 2e-3, SQ_ACTIVE_INST_VALU=1e9, SQ_THREAD_CYCLES_VALU=4e10,
+                          SQ_WAVE_CYCLES=1e9, SQ_WAIT_ANY=3e8)}
+    counters = dict(n_ret=10, n_slot=20, n_loc=30, n_cull=40, n_exact=50, n_hit=60, segments=70, primary=7)
+    kr = bench.kernel_rooflines(dur, pmc, counters)
+    w = kr["k_walk"]
+    assert w["hbm_bytes"] == 2 * 1000 * 1024 + 500 * 1024
+    cyc = 2 * (1e9 - 2e8) + 4 * 2e8
+    assert w["valu_issue_cycles"] == int(cyc)
+    assert w["clock_ghz"] == pytest.approx(2.0)
+    assert w["valu_issue_frac"] == pytest.approx(cyc / (1024 * 2.0e9 * 2e-3), rel=1e-3)
+    assert w["active_lanes"] == pytest.approx(40.0) and w["wait_frac"] == pytest.approx(0.3)
+    assert w["binding_roof"] == "valu-issue"
+    # the walk pass's algorithmic bytes are split between k_walk and k_walk_seg by time
+    walk_bytes = 48 * 10 + 32 * 20 + 40 * 30
+    assert w["alg_bytes_cache_served"] + kr["k_walk_seg"]["alg_bytes_cache_served"] == pytest.approx(walk_bytes, abs=2)
+    assert list(kr) == ["k_walk", "k_first", "k_walk_seg"]          # by time
+
+
+def test_usable_cores_reports_quota():
+    import bench
+    n, visible, quota = bench.usable_cores()
+    assert 1 <= n <= visible
+    assert quota is None or n <= quota

@@ -59,10 +59,14 @@ def test_serialize_matches_native_builder(tmp_path, name):
 def test_addon_loads_and_fails_loudly_without_gpu():
     """The addon loads; with no GPU create() throws RT_E_NODEVICE (never a silent CPU path)."""
     js = ("const rt=require(%r);const a=rt.load_addon();"
-          "if(a.abiVersion()!==3)throw Error('abi');"
-          "try{a.create(0);console.log('GPU')}catch(e){console.log(e.code)}") % os.path.join(ROOT, "raytracer.js_amd", "js", "raytracer.js")
-    out = _node(["-e", js]).strip()
-    assert out in ("GPU", "RT_E_NODEVICE")
+          "if(a.abiVersion()!==4)throw Error('abi');"
+          "try{a.create(0);console.log('GPU')}catch(e){console.log(e.code)}"
+          "try{a.create([0,0],8);console.log('GPU')}catch(e){console.log(e.code)}"
+          "try{a.create([]);console.log('empty accepted')}catch(e){console.log(e.code)}") % os.path.join(ROOT, "raytracer.js_amd", "js", "raytracer.js")
+    out = _node(["-e", js]).split()
+    assert out[0] in ("GPU", "RT_E_NODEVICE")
+    assert out[1] in ("GPU", "RT_E_NODEVICE")
+    assert out[2] == "RT_E_INVALID"
 
 
 def _textured_open(seed):
@@ -72,11 +76,15 @@ def _textured_open(seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,wh,refmax", [("config1", (256, 256), 2), ("small4", (200, 150), 3),
-                                            ("small4_rough", (200, 150), 4), ("small5_tex", (160, 120), 3)])
-def test_dropin_frame_equals_oracle(tmp_path, name, wh, refmax):
+@pytest.mark.parametrize("name,wh,refmax,devices", [("config1", (256, 256), 2, None), ("small4", (200, 150), 3, None),
+                                                    ("small4_rough", (200, 150), 4, None),
+                                                    ("small5_tex", (160, 120), 3, None),
+                                                    ("small4", (200, 150), 3, "0,0,0"),
+                                                    ("small4_rough", (200, 150), 4, "0,0")])
+def test_dropin_frame_equals_oracle(tmp_path, name, wh, refmax, devices):
     """small4_rough: rough mirrors through options.scatter = 'counter' (RT_SCATTER_COUNTER);
-    small5_tex: loaded ImageTextures on entities and the SkySphere."""
+    small5_tex: loaded ImageTextures on entities and the SkySphere; devices: the multi-device context
+    (options.devices; parts on the one GPU of the test box, gathered by device copies)."""
     spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4),
             "small4_rough": lambda: scenes.roughen(scenes.small_random(4, p_mirror=0.5)),
             "small5_tex": lambda: _textured_open(5)}[name]()
@@ -84,7 +92,8 @@ def test_dropin_frame_equals_oracle(tmp_path, name, wh, refmax):
     cam = scenes.make_camera(*wh)
     cfg = scenes.make_config(refmax, scatter_seed=seed, sky_image=2 if name.endswith("tex") else 0)
     path = _dump(tmp_path, spec, cam, cfg)
-    _node([RUNNER, path, str(tmp_path / "out")] + (["--scatter", str(seed)] if seed else []))
+    _node([RUNNER, path, str(tmp_path / "out")] + (["--scatter", str(seed)] if seed else []) +
+          (["--devices", devices] if devices else []))
     P = wh[0] * wh[1]
     rgb = np.fromfile(tmp_path / "out.rgb", dtype=np.float32)
     ent = np.fromfile(tmp_path / "out.ent", dtype=np.int32)
