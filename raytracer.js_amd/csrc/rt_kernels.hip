@@ -196,19 +196,22 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
 {
     const double hs = size * 0.5;
     const double c[3] = {cx, cy, cz};
-    double qe[3], pe[3], ae[3], qn[3], pn[3], an[3];
-    int fe[3];
+    // face 2a: p = -d, face 2a+1: p = d; isNegative(p) picks the entering one.  Only the screening
+    // products are kept; the one (normally) surviving quotient is recomputed from its axis below,
+    // with the same operations, so the live state stays small (the walker runs at 4+ waves/SIMD).
+    double ae[3];
+    double M = -INFINITY;                                // entry: u1 = first strict maximum
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         const double tl = c[a] - hs;
         const double qlo = w.o[a] - tl;
         const double qhi = tl + size - w.o[a];
-        // face 2a: p = -d, face 2a+1: p = d; isNegative(p) picks the entering one
         const bool neg = signbit(w.d[a]);
-        qe[a] = neg ? qlo : qhi;   pe[a] = neg ? -w.d[a] : w.d[a];   fe[a] = neg ? 2 * a : 2 * a + 1;
-        qn[a] = neg ? qhi : qlo;   pn[a] = neg ? w.d[a] : -w.d[a];
-        ae[a] = qe[a] * (neg ? -w.inv[a] : w.inv[a]);
-        an[a] = qn[a] * (neg ? w.inv[a] : -w.inv[a]);
+        // (neg ? -inv : inv) is |inv| (inv = RN(1/d) has d's sign; a NaN quotient never survives):
+        // the abs / neg source modifiers of the multiply, no per-ray register copies
+        ae[a] = (neg ? qlo : qhi) * fabs(w.inv[a]);
+        const double an = (neg ? qhi : qlo) * -fabs(w.inv[a]);
+        M = an > M ? an : M;
     }
     // exit: the reference keeps the first strict minimum over faces in order (u2 starts at +inf)
     double m = INFINITY;
@@ -219,8 +222,18 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
     // the common case, straight-line: one survivor of a finite minimum in the shortcut's range,
     // selected without branching so that every lane of the wave shares one division
     const bool common = fabs(m) < 1e300 && (int)s0 + (int)s1 + (int)s2 == 1;
-    double u2 = (s0 ? qe[0] : (s1 ? qe[1] : qe[2])) / (s0 ? pe[0] : (s1 ? pe[1] : pe[2]));
-    int i2 = s0 ? fe[0] : (s1 ? fe[1] : fe[2]);
+    double u2;
+    int i2;
+    {
+        const int k = s0 ? 0 : (s1 ? 1 : 2);
+        const double ck = s0 ? cx : (s1 ? cy : cz), ok = s0 ? w.o[0] : (s1 ? w.o[1] : w.o[2]);
+        const double dk = s0 ? w.d[0] : (s1 ? w.d[1] : w.d[2]);
+        const double tl = ck - hs;
+        const bool neg = signbit(dk);
+        const double q = neg ? ok - tl : tl + size - ok;
+        u2 = q / fabs(dk);                                   // (neg ? -d : d), bit for bit unless NaN
+        i2 = 2 * k + (neg ? 0 : 1);
+    }
     if (!(u2 < INFINITY)) { u2 = INFINITY; i2 = -1; }          // (a finite survivor never gets here)
     if (!common) {
         // no finite exit, |m| out of the shortcut's range (every axis exact), or several survivors
@@ -231,22 +244,23 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
 #pragma unroll
             for (int a = 0; a < 3; a++) {
                 if (all || ae[a] <= m + tol) {
-                    const double e = qe[a] / pe[a];
-                    if (e < u2) { u2 = e; i2 = fe[a]; }
+                    const double tl = c[a] - hs;
+                    const bool neg = signbit(w.d[a]);
+                    const double e = (neg ? w.o[a] - tl : tl + size - w.o[a]) / fabs(w.d[a]);
+                    if (e < u2) { u2 = e; i2 = neg ? 2 * a : 2 * a + 1; }
                 }
             }
         }
     }
-    // entry: u1 = first strict maximum (starts at -inf); only `u1 > u2` matters
-    double M = -INFINITY;
-#pragma unroll
-    for (int a = 0; a < 3; a++) M = an[a] > M ? an[a] : M;
+    // entry: only `u1 > u2` matters; divided exactly only when the screen cannot decide
     const double tolM = fabs(M) * 1.7763568394002505e-15 + 1e-300;
     if (M > -INFINITY && (!(M + tolM < u2) || !(fabs(M) < 1e300))) {
         double u1 = -INFINITY;
 #pragma unroll
         for (int a = 0; a < 3; a++) {
-            const double e = qn[a] / pn[a];
+            const double tl = c[a] - hs;
+            const bool neg = signbit(w.d[a]);
+            const double e = (neg ? tl + size - w.o[a] : w.o[a] - tl) / -fabs(w.d[a]);
             if (e > u1) u1 = e;
         }
         if (u1 > u2) return false;
@@ -347,6 +361,77 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
             if (w.depth > 0) { w.depth--; w.flags |= F_RET; }
             else w.flags &= ~F_RET;
             const RtNode &nd = S.node[w.cur_tree];             // the line update_next_pos just read
+            const int2 up = make_int2(nd.up_tree, nd.up_oct);
+            if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
+            else w.cur_oct = RT_OCT_UNDEF;
+        }
+    }
+    return 0;
+}
+
+// The whole walk of the split path's walk pass: OctreeWalker.next() called until the walk ends, every
+// returned node handed to `emit` (k_walk's candidate filter) inside the loop.  The iteration that
+// returns a node also performs what the next call's first iteration would: the step-in (or, after a
+// climb above the seat, the slot exit), so a node costs one trip of the loop instead of two and the
+// wave no longer reconverges at every return.  Visit order, throws and the step count (two per
+// returned node, as in walker_next) are those of walker_next.  Returns 0 at the end, -1 on a throw,
+// -2 at the step cap, 2 on reaching `stop` (STOP, segmented walks).
+template <bool STOP, typename Emit>
+__device__ int walker_run(const RtDevScene &S, Walker &w, Emit &&emit, int stop = -1)
+{
+    while (w.cur_tree >= 0) {
+        if (++w.steps > STEP_CAP) return -2;
+        const int ltree = w.cur_tree, loct = w.cur_oct;
+        int lnode;
+        if (loct != RT_OCT_UNDEF) {
+            if ((unsigned)loct > 7u) return -1;              // Octree.get: index out of range
+            lnode = S.node[ltree].child[loct];
+        } else {
+            lnode = ltree;
+        }
+        if (!(w.flags & F_RET) && lnode >= 0) {
+            w.flags |= F_RET;
+            emit(lnode);
+            if (++w.steps > STEP_CAP) return -2;             // the next call's first iteration
+        }
+        if (loct != RT_OCT_UNDEF) {
+            if (!(w.flags & F_AHEAD)) {
+                if (!(w.flags & F_STEPPED) && lnode >= 0) {
+                    // octant_adj_pos(node, next_pos[0]) — :41-50, then step_in — :310-314
+                    const NodeDims cd = node_dims(S, lnode);
+                    const double h = cd.s / 2;
+                    const int px = w.np[0] >= cd.x + h, py = w.np[1] >= cd.y + h, pz = w.np[2] >= cd.z + h;
+                    w.depth++;
+                    w.cur_tree = lnode;
+                    w.cur_oct = (pz << 2) | (py << 1) | px;
+                    w.flags &= ~F_RET;
+                    continue;
+                }
+                if (STOP && lnode < 0 && ltree * 8 + loct == stop) return 2;
+                Counters c_unused;
+                if (walker_update_next_pos(node_dims(S, w.cur_tree), w, c_unused) < 0) return -1;
+            }
+            if (!(w.nn & 16)) return -1;                     // vector.add(v, undefined)
+            const int face = w.nn & 7, axis = face >> 1;
+            int delta = (face & 1) ? 1 : -1;
+            if (w.nn & 8) delta = -delta;
+            const int nb = ((loct >> axis) & 1) + delta;
+            if (nb >= 0 && nb <= 1) {
+                w.cur_oct = (loct & ~(1 << axis)) | (nb << axis);
+                w.flags = 0;
+                continue;
+            }
+            w.flags |= F_AHEAD;
+        }
+        // step_back — :280-308
+        w.flags |= F_STEPPED;
+        if (w.cur_oct == RT_OCT_UNDEF) {
+            w.cur_tree = -1;
+            w.flags &= ~F_RET;
+        } else {
+            if (w.depth > 0) { w.depth--; w.flags |= F_RET; }
+            else w.flags &= ~F_RET;
+            const RtNode &nd = S.node[w.cur_tree];
             const int2 up = make_int2(nd.up_tree, nd.up_oct);
             if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
             else w.cur_oct = RT_OCT_UNDEF;
@@ -1228,18 +1313,15 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
         if (end == SEG_FIN) {
             const RayBox rb = make_raybox(w.o, w.d);
             const size_t id = (size_t)q * K + j;
-            for (;;) {
-                int node, pt, po;
-                const int r = walker_next<false, true>(S, w, node, pt, po, c, stop);
-                if (r < 0) { end = r == -2 ? SEG_CAP : SEG_THROW; break; }
-                if (r == 0) break;
-                if (r == 2) { end = SEG_REACHED; break; }
+            const int r = walker_run<true>(S, w, [&](int node) {
                 const RtNode &nd = S.node[node];
-                if (nd.n_ent == 0) continue;
-                if (L.cull && rb.ok && !ray_box(nd.box, rb)) continue;
+                if (nd.n_ent == 0) return;
+                if (L.cull && rb.ok && !ray_box(nd.box, rb)) return;
                 if (n < L.cand_cap) L.cand[(size_t)n * stride + id] = node;
                 n++;
-            }
+            }, stop);
+            if (r < 0) end = r == -2 ? SEG_CAP : SEG_THROW;
+            else if (r == 2) end = SEG_REACHED;
         }
         if (valid) L.cand_n[(size_t)q * K + j] = n > L.cand_cap ? -1 : n * 8 + end;
     }
@@ -1337,17 +1419,14 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
         if (!seated) {
             end = src.rec ? 3 : 1;
         } else {
-            for (;;) {
-                int node, pt, po;
-                const int r = walker_next<false>(S, w, node, pt, po, c);
-                if (r < 0) { end = r == -2 ? 2 : 1; break; }
-                if (r == 0) break;
-                const RtNode &nd = S.node[node];               // one cache line: count + root box
-                if (nd.n_ent == 0) continue;
-                if (L.cull && rb.ok && !ray_box(nd.box, rb)) continue;
+            const int r = walker_run<false>(S, w, [&](int node) {
+                const RtNode &nd = S.node[node];               // one cache line: count + root box + cube
+                if (nd.n_ent == 0) return;
+                if (L.cull && rb.ok && !ray_box(nd.box, rb)) return;
                 if (n < L.cand_cap) L.cand[(size_t)n * stride + src.id] = node;
                 n++;
-            }
+            });
+            if (r < 0) end = r == -2 ? 2 : 1;
         }
         L.cand_n[src.id] = n > L.cand_cap ? -1 : n * 4 + end;
     }
