@@ -13,7 +13,7 @@ int rt_set_error(int code, const char *fmt, ...);
 //   node      RtNode   128 B {pos.xyz, size, child[8], cull root box, entity count}: read by
 //                      update_next_pos / step_in / every slot visit / the walk pass's candidate test
 //   node_up   int2     {parent, index_within_parent}     read by step_back
-//   node_ent  int2     {list begin, count}               read when a node is returned
+//   node_ent  int4     {list begin, count, cull root, #within-capable}  read when a node is returned
 // Primitives are re-packed in list order (each entity appears in exactly one EntitySet), so a
 // node's entity scan streams one contiguous run of 80-byte records.
 enum : int { RT_OCT_UNDEF = -1, RT_OCT_BAD = 1000 };
@@ -71,6 +71,8 @@ struct RtDevScene {
     const RtBvh *bvh;           // [n_bvh]
     const int32_t *list_entity; // [n_list] entity id per global list index (Set order)
     const int32_t *list_prefix; // [n_list*4] per list index: #sph, #box, #tri in its node up to it (stats)
+    const int32_t *within;      // [n_list] per node region: the prim slots that can be is_within (not faces),
+                                // node_ent.w of them from the region start (entity_at_pos)
     const rt_shade *shades;     // [n_shades]
     const int32_t *ent_sub;     // [n_entities]
     const double *sub_ri;       // [n_substances]

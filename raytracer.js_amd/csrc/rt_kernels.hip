@@ -543,6 +543,8 @@ __device__ __forceinline__ bool prim_within(const RtPrim &pr, const double p[3])
 
 // entity_at_pos — src/octree_entity.ts:191-202.  Returns entity id, -1 undefined, -2 throw.
 // Prims of a node are stored in cull order, so the first entity in Set order is the minimum rank.
+// Only the node's spheres and boxes are visited (S.within): a face's is_within is false, and the
+// sets of shallow nodes hold thousands of straddling triangles (config 5's path: ~2400 per lookup).
 __device__ int entity_at_pos(const RtDevScene &S, const double p[3], long long &levels)
 {
     int t = -1, oc = 0;
@@ -552,8 +554,10 @@ __device__ int entity_at_pos(const RtDevScene &S, const double p[3], long long &
     while (cur >= 0) {
         const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[cur];
         int best = 0x7fffffff;
-        for (int k = ent.x; k < ent.x + ent.y; k++)
+        for (int j = 0; j < ent.w; j++) {
+            const int k = S.within[ent.x + j];
             if (S.prim[k].rank < best && prim_within(S.prim[k], p)) best = S.prim[k].rank;
+        }
         if (best != 0x7fffffff) return S.list_entity[best];
         cur = reinterpret_cast<const int2 *>(S.node_up)[cur].x;
     }
@@ -709,8 +713,10 @@ __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_des
         while (cur >= 0) {
             const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[cur];
             int best = 0x7fffffff;
-            for (int k = ent.x + lane; k < ent.x + ent.y; k += 64)
+            for (int j = lane; j < ent.w; j += 64) {
+                const int k = S.within[ent.x + j];
                 if (S.prim[k].rank < best && prim_within(S.prim[k], cam.pos)) best = S.prim[k].rank;
+            }
             best = wave_min(best);
             if (best != 0x7fffffff) { se = S.list_entity[best]; break; }
             cur = reinterpret_cast<const int2 *>(S.node_up)[cur].x;

@@ -42,7 +42,7 @@ int rt_build_node_cull(const RtPrim *recs, int c, int prim_base, int bvh_base, d
 namespace {
 
 enum Arr { A_NODE, A_NODE_UP, A_NODE_ENT, A_NODE_DFS, A_PRIM, A_BVH, A_LIST, A_PREFIX,
-           A_SHADES, A_ENT_SUB, A_SUB_RI, A_IMAGES, A_TEXELS, A_N };
+           A_SHADES, A_ENT_SUB, A_SUB_RI, A_IMAGES, A_TEXELS, A_WITHIN, A_N };
 
 struct DevArr {
     void *p = nullptr;
@@ -395,7 +395,7 @@ struct RtSceneStore {
         const size_t need[A_N] = {sizeof(RtNode) * n_slots, 8 * n_slots, 16 * n_slots, 4 * n_slots,
                                   sizeof(RtPrim) * list_used, sizeof(RtBvh) * bvh_used, 4 * list_used,
                                   16 * list_used, sizeof(rt_shade) * n_shades, 4 * n_ent, 8 * n_ri,
-                                  sizeof(RtImage) * n_img, n_tex};
+                                  sizeof(RtImage) * n_img, n_tex, 4 * list_used};
         for (int d = 0; d < ndev; d++) {
             HIP_TRY(hipSetDevice(devs[d]));
             for (int k = 0; k < A_N; k++) {
@@ -417,6 +417,7 @@ struct RtSceneStore {
         d.bvh = (const RtBvh *)a[A_BVH].p;
         d.list_entity = (const int32_t *)a[A_LIST].p;
         d.list_prefix = (const int32_t *)a[A_PREFIX].p;
+        d.within = (const int32_t *)a[A_WITHIN].p;
         d.shades = (const rt_shade *)a[A_SHADES].p;
         d.ent_sub = (const int32_t *)a[A_ENT_SUB].p;
         d.sub_ri = (const double *)a[A_SUB_RI].p;
@@ -442,6 +443,16 @@ struct RtSceneStore {
         m_ri.assign(s->substance_ri, s->substance_ri + s->n_substances);
     }
 
+    // The prim slots of a node's region [base, base + c) that can answer is_within (spheres and boxes;
+    // a face never contains a point), written from `out`; returns their count (node_ent.w).
+    static int within_slots(const RtPrim *prim, int c, int base, int32_t *out)
+    {
+        int w = 0;
+        for (int k = 0; k < c; k++)
+            if ((prim[k].meta & 3) != RT_ENT_FACE) out[w++] = base + k;
+        return w;
+    }
+
     // Full upload: slots in DFS order, regions packed exactly.
     int full(const rt_scene_desc *s, const std::vector<int32_t> &oct, rt_update_stats &us)
     {
@@ -464,6 +475,7 @@ struct RtSceneStore {
         std::vector<RtPrim> prim((size_t)std::max(NL, 1)), recs;
         std::vector<RtBvh> bvh(std::max<size_t>(nb, 1));
         std::vector<int32_t> prefix(4 * (size_t)std::max(NL, 1));
+        std::vector<int32_t> within((size_t)std::max(NL, 1));
         size_t lb = 0, bb = 0;
         for (int n = 0; n < N; n++) {
             RtNode &nd = m_node[n];
@@ -495,6 +507,7 @@ struct RtSceneStore {
             m_ent[4 * n] = (int32_t)lb;
             m_ent[4 * n + 1] = c;
             m_ent[4 * n + 2] = broot;
+            m_ent[4 * n + 3] = c ? within_slots(&prim[lb], c, (int)lb, &within[lb]) : 0;
             lb += c;
             bb += c ? 2 * (size_t)c - 1 : 0;
         }
@@ -508,11 +521,12 @@ struct RtSceneStore {
         if (r != RT_OK) return r;
         const void *src[A_N] = {m_node.data(), m_up.data(), m_ent.data(), m_dfs.data(), prim.data(),
                                 bvh.data(), m_list.data(), prefix.data(), s->shades, s->ent_substance, s->substance_ri,
-                                m_images.data(), m_texels.data()};
+                                m_images.data(), m_texels.data(), within.data()};
         const size_t bytes[A_N] = {sizeof(RtNode) * (size_t)N, 8 * (size_t)N, 16 * (size_t)N, 4 * (size_t)N,
                                    sizeof(RtPrim) * lb, sizeof(RtBvh) * bb, 4 * lb, 16 * lb,
                                    sizeof(rt_shade) * (size_t)s->n_shades, 4 * (size_t)s->n_entities,
-                                   8 * (size_t)s->n_substances, sizeof(RtImage) * m_images.size(), m_texels.size()};
+                                   8 * (size_t)s->n_substances, sizeof(RtImage) * m_images.size(), m_texels.size(),
+                                   4 * lb};
         for (int d = 0; d < ndev; d++) {
             HIP_TRY(hipSetDevice(devs[d]));
             for (int k = 0; k < A_N; k++) {
@@ -622,7 +636,7 @@ struct RtSceneStore {
         m_node.resize(n_slots);                       // new slots start zeroed
         std::vector<RtPrim> recs, prim;
         std::vector<RtBvh> bvh;
-        std::vector<int32_t> prefix;
+        std::vector<int32_t> prefix, wslots;
         m_ent.resize(4 * n_slots, 0);
         for (const Dirty &dd : dirty) {
             const int b = s->node_ent_begin[dd.n], c = s->node_ent_count[dd.n];
@@ -643,10 +657,13 @@ struct RtSceneStore {
             add(A_BVH, sizeof(RtBvh) * (size_t)S.bbeg, bvh.data(), sizeof(RtBvh) * bvh.size());
             add(A_LIST, 4 * (size_t)S.lbeg, &m_list[S.lbeg], 4 * (size_t)c);
             add(A_PREFIX, 16 * (size_t)S.lbeg, prefix.data(), 16 * (size_t)c);
+            wslots.resize((size_t)std::max(c, 1));
+            const int wc = c ? within_slots(prim.data(), c, S.lbeg, wslots.data()) : 0;
+            add(A_WITHIN, 4 * (size_t)S.lbeg, wslots.data(), 4 * (size_t)wc);
             m_ent[4 * dd.sl] = S.lbeg;
             m_ent[4 * dd.sl + 1] = c;
             m_ent[4 * dd.sl + 2] = S.broot;
-            m_ent[4 * dd.sl + 3] = 0;
+            m_ent[4 * dd.sl + 3] = wc;
             m_node[dd.sl].n_ent = c;
             m_node[dd.sl].ent_begin = S.lbeg;
             m_node[dd.sl].bvh_root = S.broot;
