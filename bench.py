@@ -415,8 +415,8 @@ def run_ranks(args, spec, scene, W, H, refmax, world, rank, local):
         sync()
         same = bool(same) and torch.equal(whole.view(torch.int32), sgs[0].frame.view(torch.int32))
     kt = ctx.kernel_times(args.steps)
-    extra = dict(mode="one process per GPU" if world > 1 else "one GPU", collective="torch.distributed.gather (RCCL)"
-                 if world > 1 else None, n_gpus=dist.get_world_size() if world > 1 else 1)
+    extra = dict(mode="one process per GPU" if world > 1 else "one GPU", collective="torch.distributed.gather (%s)" % (
+                 "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()) if world > 1 else None, n_gpus=dist.get_world_size() if world > 1 else 1)
     host = host_frame_time(ctx, cam, cfg, tot["segments"]) if rank == 0 and world == 1 else None
     expo = exposure_bench(ctx, sg.frame, stream) if rank == 0 else None
     out = dict(res, tot=tot, counters=counters, same=same, kernel_ms=float(np.mean(kt)) if len(kt) else None,

@@ -260,6 +260,9 @@ int  rt_update_scene(rt_ctx *ctx, const rt_scene_desc *scene, rt_update_stats *s
  * interleaved RGB); it is read (when col_weight != 1) and written.  hit_entity / hit_node
  * (W*H int32, nullable) receive the entity id / DFS node id of the primary collision, -1 for none.
  * status (W*H uint8, nullable): 0 ok, 1 acute-normal warning, 2 fault, 3 step cap.
+ * On RT_E_FAULT rgb_inout holds what the reference's ExposureBuffer holds after trace_frame throws
+ * (src/raytracer.ts:318-329): new colours for the pixels before the first throwing pixel in camera
+ * scan order (src/view/camera.ts:207-250), previous values from that pixel on.
  * On a multi-device context every device traces its stripes and the frame is assembled on
  * devices[0] before the one copy back; stats sums the devices' counters (kernel_ms: the slowest
  * device).  Synchronous, like the reference's trace_frame. */

@@ -229,10 +229,15 @@ class World:
         return out
 
     # --- frame --------------------------------------------------------------------------
-    def trace_frame(self, root, cam, cfg, pixels=None, rgb=None, nthreads=1):
+    def trace_frame(self, root, cam, cfg, pixels=None, rgb=None, nthreads=1, abort=False):
+        """abort: the reference's frame ends at its first throwing pixel (abort_at_first_throw); needs
+        the whole frame."""
         W, H = cam.width, cam.height
         P = W * H
         rgb = np.zeros(P * 3, np.float32) if rgb is None else rgb
+        if abort and pixels is not None:
+            raise ValueError("abort semantics need the whole frame")
+        old = rgb.copy() if abort else None
         hit_e = np.full(P, -7, np.int32)
         hit_n = np.full(P, -7, np.int32)
         segs = np.zeros(P, np.int32)
@@ -253,6 +258,8 @@ class World:
         if r not in (0, FAULT):
             raise RuntimeError("orc_trace_frame failed %d" % r)
         counters = dict(zip(abi.rt_stats.COUNTERS, (int(x) for x in ctr)))
+        if abort:
+            rgb[:] = abort_at_first_throw(old, rgb, status, W, H)
         return dict(rgb=rgb, hit_entity=hit_e, hit_node=hit_n, segments=segs, status=status,
                     counters=counters)
 
@@ -261,6 +268,33 @@ def camera_dirs(cam):
     out = np.zeros(cam.width * cam.height * 3)
     lib().orc_camera_dirs(C.byref(cam), out.ctypes.data_as(C.POINTER(C.c_double)))
     return out
+
+
+def scan_index(W, H):
+    """Position of every pixel (row-major y*W + x) in the order Raytracer.trace_frame writes them:
+    Camera.get_dir_for_each_pixel (src/view/camera.ts:207-250) yields rows from the centre row down,
+    then from the row above it up, and in each row the columns from the centre column right, then
+    left (rows over height, as the build scans them; tests/test_oracle_kats.py pins it to the literal
+    scan for square screens)."""
+    hh, hw = H >> 1, W >> 1
+    y, x = np.arange(H, dtype=np.int64), np.arange(W, dtype=np.int64)
+    ry = np.where(y >= hh, y - hh, (H - hh) + (hh - 1 - y))
+    rx = np.where(x >= hw, x - hw, (W - hw) + (hw - 1 - x))
+    return (ry[:, None] * W + rx[None, :]).ravel()
+
+
+def abort_at_first_throw(old_rgb, new_rgb, status, W, H):
+    """The ExposureBuffer after Raytracer.trace_frame throws (src/raytracer.ts:318-329): the loop
+    stops at the first pixel (scan order) whose Ray.trace throws, so that pixel and every later one
+    keep their previous value.  status 2 is a throw; 3 (the build's step cap) is treated as one."""
+    idx = scan_index(W, H)
+    bad = np.asarray(status).ravel() >= 2
+    if not bad.any():
+        return new_rgb
+    keep_new = idx < idx[bad].min()
+    out = np.asarray(old_rgb, np.float32).reshape(-1, 3).copy()
+    out[keep_new] = np.asarray(new_rgb, np.float32).reshape(-1, 3)[keep_new]
+    return out.ravel()
 
 
 def camera_scan_literal(cam):

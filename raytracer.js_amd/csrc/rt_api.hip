@@ -325,9 +325,12 @@ static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_confi
 
 // Per-frame buffers of device d and the launch description of one part.  The part's outputs go to
 // d.b_rgb / d.b_hit_* unless the caller repoints L.rgb.  Device d must be current.
+enum { WANT_IDS = 1, WANT_STATUS = 2 };
+
 static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_config_desc *cfg, int part,
-                   int n_parts, int stripe, bool want_ids, RtLaunch &L)
+                   int n_parts, int stripe, int want, RtLaunch &L)
 {
+    const bool want_ids = want & WANT_IDS, want_status = want & (WANT_IDS | WANT_STATUS);
     const int rows = rt_part_rows(cam->height, part, n_parts, stripe);
     const size_t P = (size_t)rows * (size_t)cam->width;
     int r;
@@ -335,8 +338,8 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     if (want_ids) {
         if ((r = d.b_hit_e.ensure(sizeof(int32_t) * (P ? P : 1))) != RT_OK) return r;
         if ((r = d.b_hit_n.ensure(sizeof(int32_t) * (P ? P : 1))) != RT_OK) return r;
-        if ((r = d.b_status.ensure(P ? P : 1)) != RT_OK) return r;
     }
+    if (want_status && (r = d.b_status.ensure(P ? P : 1)) != RT_OK) return r;
     memset(&L, 0, sizeof L);
     L.scene = d.scene;
     L.cam = *cam;
@@ -349,7 +352,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.dirs = (double *)d.b_dirs.p;
     L.hit_entity = want_ids ? (int32_t *)d.b_hit_e.p : nullptr;
     L.hit_node = want_ids ? (int32_t *)d.b_hit_n.p : nullptr;
-    L.status = want_ids ? (uint8_t *)d.b_status.p : nullptr;
+    L.status = want_status ? (uint8_t *)d.b_status.p : nullptr;
     L.fault = (int32_t *)d.b_fault.p;
     L.cull = (c->flags & RT_CREATE_NO_CULL) ? 0 : 1;
     L.ctr = (int32_t *)d.b_ctr.p;
@@ -458,7 +461,7 @@ static int frame_multi(rt_ctx *c, const rt_camera_desc *cam, const rt_config_des
         RtDevice &d = c->dev[k];
         if ((r = use_device(d)) != RT_OK) return r;
         if ((r = d.b_rgb.ensure(sizeof(float) * 3 * PS)) != RT_OK) return r;
-        if ((r = prepare(c, d, cam, cfg, k, N, stripe, ids, L[k])) != RT_OK) return r;
+        if ((r = prepare(c, d, cam, cfg, k, N, stripe, ids ? WANT_IDS : 0, L[k])) != RT_OK) return r;
         if (ids) {   // the gathered id arrays are PS long on every device
             if ((r = d.b_hit_e.ensure(sizeof(int32_t) * PS)) != RT_OK) return r;
             if ((r = d.b_hit_n.ensure(sizeof(int32_t) * PS)) != RT_OK) return r;
@@ -587,6 +590,19 @@ static int finish(rt_ctx *c, int fault_dev0_read, rt_stats *stats, std::chrono::
     return RT_OK;
 }
 
+// The reference's trace_frame (src/raytracer.ts:308-330) writes pixels in the camera's scan order
+// (Camera.get_dir_for_each_pixel, src/view/camera.ts:207-250: rows from the centre row down, then
+// up; in each row the columns from the centre column right, then left) and stops at the first pixel
+// whose Ray.trace throws: that pixel and every later one keep the ExposureBuffer's previous value.
+// Position of pixel (x, y) in that order (rows over height):
+static inline int64_t scan_index(int x, int y, int W, int H)
+{
+    const int hh = H >> 1, hw = W >> 1;
+    const int64_t ry = y >= hh ? y - hh : (H - hh) + (hh - 1 - y);
+    const int64_t rx = x >= hw ? x - hw : (W - hw) + (hw - 1 - x);
+    return ry * W + rx;
+}
+
 extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,
                               int32_t *hit_entity, int32_t *hit_node, uint8_t *status, rt_stats *stats)
 {
@@ -597,14 +613,15 @@ extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     DevGuard guard;
     RtDevice &d0 = c->dev[0];
     if ((r = use_device(d0)) != RT_OK) return r;
-    const int H = cam->height;
-    const bool ids = hit_entity || hit_node || status;
-    const size_t P = (size_t)cam->width * (size_t)H;
+    const int W = cam->width, H = cam->height;
+    const bool ids = hit_entity || hit_node;
+    const size_t P = (size_t)W * (size_t)H;
     const bool blend = cfg->col_weight != 1.0;
     FrameOut o = {};
     if (c->gather == RT_GATHER_NONE) {
         RtLaunch L;
-        if ((r = prepare(c, d0, cam, cfg, 0, 1, H, ids, L)) != RT_OK) return r;
+        // per-pixel status always: it locates the first throwing pixel of a faulting frame
+        if ((r = prepare(c, d0, cam, cfg, 0, 1, H, WANT_STATUS | (ids ? WANT_IDS : 0), L)) != RT_OK) return r;
         if ((r = d0.b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
         L.rgb = (float *)d0.b_rgb.p;
         if (blend) HIP_TRY(hipMemcpyAsync(L.rgb, rgb_inout, sizeof(float) * 3 * P, hipMemcpyHostToDevice, d0.stream));
@@ -618,26 +635,52 @@ extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_con
         o = {L.rgb, L.hit_entity, L.hit_node, L.status};
     } else {
         if ((r = c->g_frame.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
-        o.rgb = (float *)c->g_frame.p;
-        if (ids) {
-            if ((r = c->g_hit_e.ensure(sizeof(int32_t) * P)) != RT_OK) return r;
-            if ((r = c->g_hit_n.ensure(sizeof(int32_t) * P)) != RT_OK) return r;
-            if ((r = c->g_status.ensure(P)) != RT_OK) return r;
-            o.hit_e = (int32_t *)c->g_hit_e.p;
-            o.hit_n = (int32_t *)c->g_hit_n.p;
-            o.status = (uint8_t *)c->g_status.p;
-        }
+        if ((r = c->g_hit_e.ensure(sizeof(int32_t) * P)) != RT_OK) return r;
+        if ((r = c->g_hit_n.ensure(sizeof(int32_t) * P)) != RT_OK) return r;
+        if ((r = c->g_status.ensure(P)) != RT_OK) return r;
+        o = {(float *)c->g_frame.p, (int32_t *)c->g_hit_e.p, (int32_t *)c->g_hit_n.p, (uint8_t *)c->g_status.p};
         if (blend) HIP_TRY(hipMemcpyAsync(o.rgb, rgb_inout, sizeof(float) * 3 * P, hipMemcpyHostToDevice, d0.stream));
         if ((r = frame_multi(c, cam, cfg, o, nullptr, stats != nullptr)) != RT_OK) return r;
-        HIP_TRY(hipSetDevice(d0.device));
     }
-    HIP_TRY(hipMemcpyAsync(rgb_inout, o.rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost, d0.stream));
+    int fault = 0;
+    if ((r = finish(c, 0, stats, t0, &fault)) != RT_OK) return r;     // every device done; faults, counters
+    HIP_TRY(hipSetDevice(d0.device));
+    std::vector<uint8_t> st_tmp;
+    uint8_t *st_host = status;
+    if (fault && !st_host) {
+        st_tmp.resize(P);
+        st_host = st_tmp.data();
+    }
+    std::vector<float> fresh;
+    float *rgb_dst = rgb_inout;
+    if (fault) {
+        fresh.resize(3 * P);
+        rgb_dst = fresh.data();
+    }
+    HIP_TRY(hipMemcpyAsync(rgb_dst, o.rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost, d0.stream));
     if (hit_entity) HIP_TRY(hipMemcpyAsync(hit_entity, o.hit_e, sizeof(int32_t) * P, hipMemcpyDeviceToHost, d0.stream));
     if (hit_node) HIP_TRY(hipMemcpyAsync(hit_node, o.hit_n, sizeof(int32_t) * P, hipMemcpyDeviceToHost, d0.stream));
-    if (status) HIP_TRY(hipMemcpyAsync(status, o.status, P, hipMemcpyDeviceToHost, d0.stream));
-    int fault = 0;
-    if ((r = finish(c, 0, stats, t0, &fault)) != RT_OK) return r;
-    if (fault) return rt_set_error(RT_E_FAULT, "a ray reached a state where the reference throws (status 2/3 pixels)");
+    if (st_host) HIP_TRY(hipMemcpyAsync(st_host, o.status, P, hipMemcpyDeviceToHost, d0.stream));
+    HIP_TRY(hipStreamSynchronize(d0.stream));
+    if (fault) {
+        // the reference's frame ends at its first throwing pixel (status 2; a step-capped ray, 3,
+        // counts as one): earlier pixels take the new colour, it and later ones keep the old
+        int64_t first = (int64_t)P;
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++)
+                if (st_host[(size_t)y * W + x] >= 2) first = std::min(first, scan_index(x, y, W, H));
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++)
+                if (scan_index(x, y, W, H) < first) {
+                    const size_t i = 3 * ((size_t)y * W + x);
+                    rgb_inout[i] = fresh[i];
+                    rgb_inout[i + 1] = fresh[i + 1];
+                    rgb_inout[i + 2] = fresh[i + 2];
+                }
+    }
+    if (stats) stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (fault) return rt_set_error(RT_E_FAULT, "a ray reached a state where the reference throws (status 2/3 pixels); "
+                                               "pixels from the first one in scan order on keep their previous value");
     return RT_OK;
 }
 
@@ -653,7 +696,7 @@ extern "C" int rt_trace_frame_device(rt_ctx *c, const rt_camera_desc *cam, const
     hipStream_t st = stream ? (hipStream_t)stream : d0.stream;
     if (c->gather == RT_GATHER_NONE) {
         RtLaunch L;
-        if ((r = prepare(c, d0, cam, cfg, 0, 1, cam->height, false, L)) != RT_OK) return r;
+        if ((r = prepare(c, d0, cam, cfg, 0, 1, cam->height, 0, L)) != RT_OK) return r;
         L.rgb = d_rgb;
         HIP_TRY(hipMemsetAsync(d0.b_fault.p, 0, sizeof(int), st));
         hipEvent_t *ev = next_events(d0);
@@ -693,7 +736,7 @@ extern "C" int rt_trace_rows_device(rt_ctx *c, const rt_camera_desc *cam, const 
     RtDevice &d0 = c->dev[0];
     if ((r = use_device(d0)) != RT_OK) return r;
     RtLaunch L;
-    if ((r = prepare(c, d0, cam, cfg, part, n_parts, stripe_rows, false, L)) != RT_OK) return r;
+    if ((r = prepare(c, d0, cam, cfg, part, n_parts, stripe_rows, 0, L)) != RT_OK) return r;
     if (rows_out) *rows_out = L.rows;
     if (!d_rgb && L.rows > 0) return rt_set_error(RT_E_INVALID, "rt_trace_rows_device: d_rgb is null");
     hipStream_t st = stream ? (hipStream_t)stream : d0.stream;
@@ -841,7 +884,7 @@ extern "C" int rt_debug_camera_dirs(rt_ctx *c, const rt_camera_desc *cam, double
     cfg.default_substance = -1;
     cfg.col_weight = 1;
     RtLaunch L;
-    if ((r = prepare(c, d0, cam, &cfg, 0, 1, cam->height, false, L)) != RT_OK) return r;
+    if ((r = prepare(c, d0, cam, &cfg, 0, 1, cam->height, 0, L)) != RT_OK) return r;
     const size_t P = (size_t)cam->width * (size_t)cam->height;
     if ((r = d0.b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
     L.rgb = (float *)d0.b_rgb.p;

@@ -181,6 +181,35 @@ def test_frame_fault_reports_reference_throws():
             m.close()
 
 
+@pytest.mark.parametrize("kw", [dict(device=0), dict(devices=[0, 0, 0], stripe_rows=3)])
+def test_throw_keeps_the_reference_partial_frame(kw):
+    """After a throw the reference's ExposureBuffer holds the pixels traced before the first throwing
+    pixel in scan order; that pixel and all later ones keep their previous value
+    (src/raytracer.ts:318-329).  rt_trace_frame leaves the same buffer, bit for bit with the oracle."""
+    spec = _throwing_scene()
+    cam, cfg = scenes.make_camera(96, 72), scenes.make_config(5, default_substance=-1, col_weight=0.5)
+    old = np.random.default_rng(5).random(96 * 72 * 3, dtype=np.float32)
+    w, root = oracle.build_scene(spec)
+    try:
+        want = w.trace_frame(root, cam, cfg, rgb=old.copy(), abort=True)
+    finally:
+        w.close()
+    st = want["status"]
+    assert (st == 2).any() and (st == 0).any()
+    m = _ctx(rtamd.build_scene(spec), **kw)
+    try:
+        got = m.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True)
+    finally:
+        m.close()
+    assert got["rc"] == abi.RT_E_FAULT
+    assert np.array_equal(got["status"], st)
+    assert np.array_equal(got["rgb"].view(np.uint32), want["rgb"].view(np.uint32))
+    idx = oracle.scan_index(96, 72)
+    kept = idx >= idx[st.ravel() >= 2].min()
+    assert kept.any() and (~kept).any()
+    assert np.array_equal(got["rgb"].reshape(-1, 3)[kept], old.reshape(-1, 3)[kept])
+
+
 def test_config3_split_over_parts():
     """BASELINE config 3 at 1920x1080 as 4 parts: bit-identical to the one-part frame."""
     factory, W, H, refmax = scenes.WORKLOADS["config3"]

@@ -147,3 +147,27 @@ def test_camera_generator_order_center_pixel():
     xs, ys, d = oracle.camera_scan_literal(cam)
     assert (xs[0], ys[0]) == (16, 16)
     assert tuple(d[0]) == tuple(cam.fr)
+
+
+@pytest.mark.parametrize("wh", [(8, 8), (9, 9), (16, 16)])
+def test_scan_index_is_the_reference_scan_order(wh):
+    """oracle.scan_index (the order trace_frame writes pixels, used for the abort at the first
+    throwing pixel) equals the literal Camera.get_dir_for_each_pixel order on square screens."""
+    cam = scenes.make_camera(*wh)
+    xs, ys, _ = oracle.camera_scan_literal(cam)
+    idx = oracle.scan_index(cam.width, cam.height)
+    assert np.array_equal(idx[ys.astype(np.int64) * cam.width + xs], np.arange(cam.width * cam.height))
+
+
+def test_abort_at_first_throw_keeps_later_pixels():
+    W, H = 6, 4
+    old = np.arange(W * H * 3, dtype=np.float32)
+    new = -old - 1
+    st = np.zeros(W * H, np.uint8)
+    st[1 * W + 5] = 2                      # a throw at (5, 1): scan position ry(1)=2 -> 2*6 + rx(5)=2 = 14
+    out = oracle.abort_at_first_throw(old, new, st, W, H).reshape(-1, 3)
+    idx = oracle.scan_index(W, H)
+    assert idx[1 * W + 5] == 14
+    assert np.array_equal(out[idx < 14], new.reshape(-1, 3)[idx < 14])
+    assert np.array_equal(out[idx >= 14], old.reshape(-1, 3)[idx >= 14])
+    assert oracle.abort_at_first_throw(old, new, np.zeros(W * H, np.uint8), W, H) is new
