@@ -103,7 +103,6 @@ struct rt_ctx {
     int seg = 8;                     // segments per bounce ray, levels >= 1 (RT_SEG: 0/1 off, 2..64)
     int occ = 0;
     int diag = 0;
-    int walk_sync = 1;               // walker_run sync_min (RT_SYNC)
     bool has_scene = false;
     bool scatter = false;            // a mirror shade with roughness > 0 is reachable
     RtSceneStore *store = nullptr;   // the resident scene (rt_scene.hip), replicated on every device
@@ -177,7 +176,6 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_SEG")) c->seg = atoi(e) > 1 ? pow2_at_most_64(atoi(e)) : 0;
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
-    if (const char *e = getenv("RT_SYNC")) c->walk_sync = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
     // parts on one GPU) gathers by device copies, as RT_CREATE_PEER_GATHER asks for.  RT_GATHER
     // (rccl / peer) forces a mode, also for one device (tests on a one-GPU host).
@@ -364,7 +362,6 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.xcd_mask = c->xcd_mask;
     L.shade_occ = c->shade_occ;
     L.seg = c->seg;
-    L.walk_sync = c->walk_sync;
     L.blend = cfg->col_weight != 1.0;
     if (c->split && P > 0) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot

@@ -146,7 +146,6 @@ struct RtLaunch {
     int32_t shade_occ;                          // k_shade waves per SIMD the registers must admit (3, 4, 5)
     int32_t seg;                                // segments per bounce ray, levels >= 1 (0: off; RT_SEG; §5.10)
     int32_t *ray_cn;                            // device [rows*W]: per-ray status of a segmented level
-    int32_t walk_sync;                          // walker_run: lanes that must wait for a slot exit before it runs
 };
 
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };

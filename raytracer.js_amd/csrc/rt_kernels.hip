@@ -377,54 +377,62 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
 // returned node, as in walker_next) are those of walker_next.  Returns 0 at the end, -1 on a throw,
 // -2 at the step cap, 2 on reaching `stop` (STOP, segmented walks).
 //
-// A reference iteration that needs the slot exit (update_next_pos, the binary64 part) is split in
-// two: its head (step count, the slot's node, the STOP check) and the exit with the move that
-// follows it.  The exit runs in a trip where at least `sync_min` lanes of the wave (or every live
-// lane) wait for one, so the expensive block executes for many lanes at once while the others keep
-// taking their cheap steps.  sync_min = 1 runs every exit in the trip of its head.  A lane's own
-// sequence of operations is unchanged: results are identical for every sync_min.
+// Each trip classifies every walking lane by what its reference iteration does next — a step-in, a
+// slot exit (update_next_pos, the binary64 part), or a move along next_pos's normal (sibling or
+// step_back) — and runs each kind once for all its lanes: the step-in and the slot exit share one
+// cube load (of the entered node, or of the slot's parent), and a slot exit falls through into the
+// same move block the F_AHEAD lanes run.  Lanes in different phases of their walks therefore no
+// longer pay for two copies of the move and two cube loads per trip.
 template <bool STOP, typename Emit>
-__device__ int walker_run(const RtDevScene &S, Walker &w, Emit &&emit, int stop = -1, int sync_min = 1)
+__device__ int walker_run(const RtDevScene &S, Walker &w, Emit &&emit, int stop = -1)
 {
-    int res = w.cur_tree >= 0 ? 1 : 0;   // 1 while walking, else the result
-    bool wait_exit = false;              // the head of a slot-exit iteration ran; the exit is pending
+    enum : int { A_NONE = 0, A_STEPIN = 1, A_EXIT = 2, A_MOVE = 3 };
+    int res = w.cur_tree >= 0 ? 1 : 0;
     for (;;) {
-        if (res == 1 && !wait_exit) {
-            // ---- one reference iteration, up to its slot exit
-            for (;;) {
-                if (++w.steps > STEP_CAP) { res = -2; break; }
-                const int ltree = w.cur_tree, loct = w.cur_oct;
-                int lnode;
-                if (loct != RT_OCT_UNDEF) {
-                    if ((unsigned)loct > 7u) { res = -1; break; }          // Octree.get: index out of range
-                    lnode = S.node[ltree].child[loct];
-                } else {
-                    lnode = ltree;
-                }
+        int act = A_NONE, lnode = -1;
+        if (res == 1) {
+            const int ltree = w.cur_tree, loct = w.cur_oct;
+            if (++w.steps > STEP_CAP) {
+                res = -2;
+            } else if (loct != RT_OCT_UNDEF && (unsigned)loct > 7u) {
+                res = -1;                                          // Octree.get: index out of range
+            } else {
+                lnode = loct != RT_OCT_UNDEF ? S.node[ltree].child[loct] : ltree;
                 if (!(w.flags & F_RET) && lnode >= 0) {
                     w.flags |= F_RET;
                     emit(lnode);
-                    if (++w.steps > STEP_CAP) { res = -2; break; }         // the next call's first iteration
+                    if (++w.steps > STEP_CAP) res = -2;            // the next call's first iteration
                 }
-                if (loct == RT_OCT_UNDEF) { res = 0; break; }              // step_back from the tree's own slot
-                if (!(w.flags & F_AHEAD)) {
-                    if (!(w.flags & F_STEPPED) && lnode >= 0) {
-                        // octant_adj_pos(node, next_pos[0]) — :41-50, then step_in — :310-314
-                        const NodeDims cd = node_dims(S, lnode);
-                        const double h = cd.s / 2;
-                        const int px = w.np[0] >= cd.x + h, py = w.np[1] >= cd.y + h, pz = w.np[2] >= cd.z + h;
-                        w.depth++;
-                        w.cur_tree = lnode;
-                        w.cur_oct = (pz << 2) | (py << 1) | px;
-                        w.flags &= ~F_RET;
-                        break;
-                    }
-                    if (STOP && lnode < 0 && ltree * 8 + loct == stop) { res = 2; break; }
-                    wait_exit = true;                                      // update_next_pos, below
-                    break;
+                if (res == 1) {
+                    if (loct == RT_OCT_UNDEF) res = 0;             // step_back from the tree's own slot
+                    else if (w.flags & F_AHEAD) act = A_MOVE;      // next_pos stands; the same normal again
+                    else if (!(w.flags & F_STEPPED) && lnode >= 0) act = A_STEPIN;
+                    else if (STOP && lnode < 0 && ltree * 8 + loct == stop) res = 2;
+                    else act = A_EXIT;
                 }
-                // F_AHEAD: next_pos stands; the same normal moves again (after a step_back)
-                if (!(w.nn & 16)) { res = -1; break; }                    // vector.add(v, undefined)
+            }
+        }
+        if (act == A_STEPIN || act == A_EXIT) {
+            const NodeDims cd = node_dims(S, act == A_STEPIN ? lnode : w.cur_tree);
+            if (act == A_STEPIN) {
+                // octant_adj_pos(node, next_pos[0]) — :41-50, then step_in — :310-314
+                const double h = cd.s / 2;
+                const int px = w.np[0] >= cd.x + h, py = w.np[1] >= cd.y + h, pz = w.np[2] >= cd.z + h;
+                w.depth++;
+                w.cur_tree = lnode;
+                w.cur_oct = (pz << 2) | (py << 1) | px;
+                w.flags &= ~F_RET;
+            } else {
+                Counters c_unused;
+                if (walker_update_next_pos(cd, w, c_unused) < 0) res = -1;
+                else act = A_MOVE;
+            }
+        }
+        if (act == A_MOVE) {
+            const int loct = w.cur_oct;
+            if (!(w.nn & 16)) {
+                res = -1;                                          // vector.add(v, undefined)
+            } else {
                 const int face = w.nn & 7, axis = face >> 1;
                 int delta = (face & 1) ? 1 : -1;
                 if (w.nn & 8) delta = -delta;
@@ -433,7 +441,7 @@ __device__ int walker_run(const RtDevScene &S, Walker &w, Emit &&emit, int stop 
                     w.cur_oct = (loct & ~(1 << axis)) | (nb << axis);
                     w.flags = 0;
                 } else {
-                    w.flags |= F_AHEAD | F_STEPPED;                        // step_back — :280-308
+                    w.flags |= F_AHEAD | F_STEPPED;                // step_back — :280-308
                     if (w.depth > 0) { w.depth--; w.flags |= F_RET; }
                     else w.flags &= ~F_RET;
                     const RtNode &nd = S.node[w.cur_tree];
@@ -441,37 +449,9 @@ __device__ int walker_run(const RtDevScene &S, Walker &w, Emit &&emit, int stop 
                     if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
                     else w.cur_oct = RT_OCT_UNDEF;
                 }
-                break;
-            }
-            if (res == 1 && w.cur_tree < 0) res = 0;
-        }
-        const unsigned long long m_live = __ballot(res == 1), m_wait = __ballot(res == 1 && wait_exit);
-        if (!m_live) break;
-        const bool run = __popcll(m_wait) >= sync_min || m_wait == m_live;
-        if (run && res == 1 && wait_exit) {
-            // ---- the slot exit and the move it leads to
-            wait_exit = false;
-            const int loct = w.cur_oct;
-            Counters c_unused;
-            if (walker_update_next_pos(node_dims(S, w.cur_tree), w, c_unused) < 0) { res = -1; continue; }
-            if (!(w.nn & 16)) { res = -1; continue; }                      // vector.add(v, undefined)
-            const int face = w.nn & 7, axis = face >> 1;
-            int delta = (face & 1) ? 1 : -1;
-            if (w.nn & 8) delta = -delta;
-            const int nb = ((loct >> axis) & 1) + delta;
-            if (nb >= 0 && nb <= 1) {
-                w.cur_oct = (loct & ~(1 << axis)) | (nb << axis);
-                w.flags = 0;
-            } else {
-                w.flags |= F_AHEAD | F_STEPPED;                            // step_back — :280-308
-                if (w.depth > 0) { w.depth--; w.flags |= F_RET; }
-                else w.flags &= ~F_RET;
-                const RtNode &nd = S.node[w.cur_tree];
-                const int2 up = make_int2(nd.up_tree, nd.up_oct);
-                if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
-                else w.cur_oct = RT_OCT_UNDEF;
             }
         }
+        if (!__ballot(res == 1)) break;
     }
     return res;
 }
@@ -1355,13 +1335,14 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
         if (end == SEG_FIN) {
             const RayBox rb = make_raybox(w.o, w.d);
             const size_t id = (size_t)q * K + j;
-            const int r = walker_run<true>(S, w, [&](int node) {
+            auto emit = [&](int node) {
                 const RtNode &nd = S.node[node];
                 if (nd.n_ent == 0) return;
                 if (L.cull && rb.ok && !ray_box(nd.box, rb)) return;
                 if (n < L.cand_cap) L.cand[(size_t)n * stride + id] = node;
                 n++;
-            }, stop, L.walk_sync);
+            };
+            const int r = walker_run<true>(S, w, emit, stop);
             if (r < 0) end = r == -2 ? SEG_CAP : SEG_THROW;
             else if (r == 2) end = SEG_REACHED;
         }
@@ -1461,13 +1442,14 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
         if (!seated) {
             end = src.rec ? 3 : 1;
         } else {
-            const int r = walker_run<false>(S, w, [&](int node) {
+            auto emit = [&](int node) {
                 const RtNode &nd = S.node[node];               // one cache line: count + root box + cube
                 if (nd.n_ent == 0) return;
                 if (L.cull && rb.ok && !ray_box(nd.box, rb)) return;
                 if (n < L.cand_cap) L.cand[(size_t)n * stride + src.id] = node;
                 n++;
-            }, -1, L.walk_sync);
+            };
+            const int r = walker_run<false>(S, w, emit);
             if (r < 0) end = r == -2 ? 2 : 1;
         }
         L.cand_n[src.id] = n > L.cand_cap ? -1 : n * 4 + end;
