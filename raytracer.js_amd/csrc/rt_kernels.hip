@@ -382,7 +382,8 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
 // step_back) — and runs each kind once for all its lanes: the step-in and the slot exit share one
 // cube load (of the entered node, or of the slot's parent), and a slot exit falls through into the
 // same move block the F_AHEAD lanes run.  Lanes in different phases of their walks therefore no
-// longer pay for two copies of the move and two cube loads per trip.
+// longer pay for two copies of the move and two cube loads per trip.  The slot's
+// parent link is read with its child id (one line), so a step_back does not wait for a load.
 template <bool STOP, typename Emit>
 __device__ int walker_run(const RtDevScene &S, Walker &w, Emit &&emit, int stop = -1)
 {
@@ -390,6 +391,7 @@ __device__ int walker_run(const RtDevScene &S, Walker &w, Emit &&emit, int stop 
     int res = w.cur_tree >= 0 ? 1 : 0;
     for (;;) {
         int act = A_NONE, lnode = -1;
+        int2 up = make_int2(-1, RT_OCT_UNDEF);
         if (res == 1) {
             const int ltree = w.cur_tree, loct = w.cur_oct;
             if (++w.steps > STEP_CAP) {
@@ -397,7 +399,13 @@ __device__ int walker_run(const RtDevScene &S, Walker &w, Emit &&emit, int stop 
             } else if (loct != RT_OCT_UNDEF && (unsigned)loct > 7u) {
                 res = -1;                                          // Octree.get: index out of range
             } else {
-                lnode = loct != RT_OCT_UNDEF ? S.node[ltree].child[loct] : ltree;
+                if (loct != RT_OCT_UNDEF) {
+                    const RtNode &tn = S.node[ltree];
+                    lnode = tn.child[loct];
+                    up = make_int2(tn.up_tree, tn.up_oct);        // step_back's parent link, same line
+                } else {
+                    lnode = ltree;
+                }
                 if (!(w.flags & F_RET) && lnode >= 0) {
                     w.flags |= F_RET;
                     emit(lnode);
@@ -444,8 +452,6 @@ __device__ int walker_run(const RtDevScene &S, Walker &w, Emit &&emit, int stop 
                     w.flags |= F_AHEAD | F_STEPPED;                // step_back — :280-308
                     if (w.depth > 0) { w.depth--; w.flags |= F_RET; }
                     else w.flags &= ~F_RET;
-                    const RtNode &nd = S.node[w.cur_tree];
-                    const int2 up = make_int2(nd.up_tree, nd.up_oct);
                     if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
                     else w.cur_oct = RT_OCT_UNDEF;
                 }
