@@ -32,8 +32,9 @@ Prints ONE JSON line on rank 0.  Beside `value` it reports:
                 labelled so); the headline entry is the dominant kernel against the roof that binds.
   host_frame    rt_trace_frame (host Float32Array in and out, what the JS drop-in calls): median
                 wall time of 10 frames after 3 warm-ups (SURVEY §8(d) ms/frame), PCIe included.
-  cpu_baseline  the oracle restatement (plain C) on a bounded pixel sample, 1 thread and all the
-                cores this process may use, with the host CPU model.
+  cpu_baseline  the path restated in JavaScript (oracle/js/rt_path.js, the reference's object model) on
+                node: a bounded pixel sample on 1 thread and a worker_threads split over all the cores
+                this process may use, with the host CPU model; the C oracle's timing beside it.
 """
 import os
 
@@ -124,7 +125,7 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(spec, cam, cfg, budget_s):
+def cpu_baseline_c(spec, cam, cfg, budget_s):
     """Oracle restatement (plain C) on a random pixel sample: 1 thread for ~budget_s, then the same
     sample on every usable core.  Mrays/s of traced segments."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -147,13 +148,59 @@ def cpu_baseline(spec, cam, cfg, budget_s):
     r = w.trace_frame(root, cam, cfg, pixels=order[:done], nthreads=nt)
     t_mt = time.perf_counter() - t0
     w.close()
-    model = cpu_model()
     return dict(value=segs / t_used / 1e6, unit="Mrays/s", cores=1, kind="port",
                 sample="%d random pixels of the %dx%d frame (%d segments) in %.1f s, oracle/rt_oracle.c, 1 thread"
                        % (done, cam.width, cam.height, segs, t_used),
-                cpu_model=model, cpus_visible=visible, cpu_quota=quota,
                 threaded=dict(value=r["counters"]["segments"] / t_mt / 1e6, unit="Mrays/s", cores=nt,
                               sample="the same pixels on %d threads (all usable cores), %.2f s" % (nt, t_mt)))
+
+
+def cpu_baseline_js(scene, cam, cfg, budget_s):
+    """The path restated in JavaScript on the reference's object model (oracle/js/rt_path.js), run by
+    node: 1 thread on a random pixel sample sized for ~budget_s, then a worker_threads split of a
+    larger sample over every usable core (BASELINE.md CPU-baseline plan).  Bit-identical to the C
+    oracle (tests/test_js_baseline.py).  None when node is absent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import js_baseline
+    if js_baseline.node_binary() is None:
+        return None
+    P = cam.width * cam.height
+    order = np.random.default_rng(1).permutation(P).astype(np.int32)
+    tmp = tempfile.mkdtemp(prefix="rt_jsb_")
+    try:
+        js_baseline.export(scene, cam, cfg, order[:4096], tmp)            # calibration (JIT warm-up included)
+        info, _ = js_baseline.run(tmp, threads=1)
+        rate = max(info["segments"] / info["trace_s"], 1.0)
+        n1 = int(min(P, max(4096, rate * budget_s)))
+        js_baseline.export(scene, cam, cfg, order[:n1], tmp)
+        i1, _ = js_baseline.run(tmp, threads=1, timeout=max(120, 6 * budget_s))
+        nt, visible, quota = usable_cores()
+        nm = int(min(P, max(n1, rate * budget_s * nt / 2)))
+        js_baseline.export(scene, cam, cfg, order[:nm], tmp)
+        im, _ = js_baseline.run(tmp, threads=nt, timeout=max(120, 6 * budget_s))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return dict(value=i1["segments"] / i1["trace_s"] / 1e6, unit="Mrays/s", cores=1, kind="port",
+                language="JavaScript, node %s (V8)" % i1["node"],
+                sample="%d random pixels of the %dx%d frame (%d segments) in %.1f s, oracle/js/rt_path.js, 1 thread"
+                       % (i1["pixels"], cam.width, cam.height, i1["segments"], i1["trace_s"]),
+                threaded=dict(value=im["segments"] / im["trace_s"] / 1e6, unit="Mrays/s", cores=nt,
+                              sample="%d random pixels (%d segments) over %d worker_threads, %.2f s"
+                                     % (im["pixels"], im["segments"], nt, im["trace_s"])),
+                node_os_cpus=i1["cpus"])
+
+
+def cpu_baseline(spec, scene, cam, cfg, budget_s):
+    """cpu_baseline: the JavaScript restatement on node (the reference's own language and object
+    model) when node is present, with the C oracle's timing beside it under `c_oracle`."""
+    nt, visible, quota = usable_cores()
+    js = cpu_baseline_js(scene, cam, cfg, budget_s / 2)
+    c = cpu_baseline_c(spec, cam, cfg, budget_s / 2 if js else budget_s)
+    out = js if js else c
+    out.update(cpu_model=cpu_model(), cpus_visible=visible, cpu_quota=quota)
+    if js:
+        out["c_oracle"] = c
+    return out
 
 
 # ---- rocprofv3 passes (N = 1) ------------------------------------------------------------------------
@@ -505,7 +552,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="config3", choices=sorted(scenes.WORKLOADS))
     ap.add_argument("--stripe", type=int, default=8, help="rows per stripe of the row-interleaved split")
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle CPU work (0 = skip)")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work (0 = skip)")
     ap.add_argument("--no-traffic", "--no-profile", dest="no_profile", action="store_true",
                     help="skip the rocprofv3 kernel-trace / PMC passes")
     ap.add_argument("--profile-out", default=None, help="keep the rocprofv3 summaries (kernel stats, PMC) here")
@@ -580,7 +627,7 @@ def main():
         if err or notes:
             roofline["profile_notes"] = [x for x in [err] + notes if x]
 
-    cpu = cpu_baseline(spec, cam, cfg, args.cpu_budget) if args.cpu_budget > 0 and n_gpus == 1 else None
+    cpu = cpu_baseline(spec, scene, cam, cfg, args.cpu_budget) if args.cpu_budget > 0 and n_gpus == 1 else None
     rec = {
         "metric": "Mrays/s (whole node) at %dx%d" % (W, H),
         "value": round(value, 3),
