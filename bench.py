@@ -45,6 +45,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
 
 import argparse
 import csv
+import datetime
 import glob
 import json
 import math
@@ -400,7 +401,9 @@ def run_ranks(args, spec, scene, W, H, refmax, world, rank, local):
     dev = torch.device("cuda", local)
     if world > 1:
         backend = os.environ.get("RT_BENCH_BACKEND", "nccl")   # "gloo": plumbing checks with ranks sharing a GPU
-        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
+        # a bounded timeout: a collective that never completes fails the run instead of hanging it
+        dist.init_process_group(backend, timeout=datetime.timedelta(minutes=5),
+                                **({"device_id": dev} if backend == "nccl" else {}))
         if dist.get_world_size() != args.gpus:
             fail("torch.distributed world size %d != --gpus %d" % (dist.get_world_size(), args.gpus))
     P = max(1, min(args.inflight or 16, args.steps))
