@@ -370,6 +370,16 @@ int  rt_builder_set_shade(rt_builder *b, int32_t entity_id, int32_t shade, int32
  * `out` stay valid until the next rt_builder_* call on `b`. */
 int  rt_builder_desc(rt_builder *b, const rt_shade *shades, int32_t n_shades,
                      const double *substance_ri, int32_t n_substances, rt_scene_desc *out);
+/* Make ctx's resident scene the builder's current tree, sending only what the builder's edits
+ * since its last sync with ctx changed (add_entity_to_octree, Entity._set_pos + set_octree,
+ * set_material, src/octree_entity.ts:174-188, src/entity.ts:50-56): O(edit) on the host, with no
+ * linearisation and no diff of the whole scene (rt_builder_desc + rt_update_scene cost O(scene)).
+ * The first sync, a sync after any other upload to ctx, an edit the journal cannot express (the
+ * tree grew above its root) or mostly-garbage pools fall back to rt_builder_desc + a full upload
+ * (stats->full = 1).  Frames equal rt_upload_scene(rt_builder_desc(b)) bit for bit.  Synchronises
+ * ctx's devices first: no frame may be in flight. */
+int  rt_builder_sync(rt_ctx *ctx, rt_builder *b, const rt_shade *shades, int32_t n_shades,
+                     const double *substance_ri, int32_t n_substances, rt_update_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -300,6 +300,44 @@ extern "C" int rt_update_scene(rt_ctx *c, const rt_scene_desc *s, rt_update_stat
     return upload(c, s, true, stats);
 }
 
+extern "C" int rt_builder_sync(rt_ctx *c, rt_builder *b, const rt_shade *shades, int32_t n_shades,
+                               const double *substance_ri, int32_t n_substances, rt_update_stats *stats)
+{
+    if (!c || !b || n_shades < 0 || n_substances < 0 || (n_shades && !shades) || (n_substances && !substance_ri))
+        return rt_set_error(RT_E_INVALID, "rt_builder_sync: bad argument");
+    for (int i = 0; i < n_shades; i++)
+        if (shades[i].image != 0)        // image tables travel with a desc (rt_update_scene)
+            return rt_set_error(RT_E_UNSUPPORTED, "rt_builder_sync: shade %d has an image texture", i);
+    DevGuard guard;
+    if (c->has_scene) {
+        RtEdit e;
+        int r = rt_builder_edit(b, c->store, rt_store_epoch(c->store), shades, n_shades, e);
+        if (r < 0) return r;
+        if (r == 0) {
+            RtDevScene scenes[RT_MAX_DEVICES];
+            c->has_scene = false;
+            r = rt_store_apply_edit(c->store, e, shades, n_shades, substance_ri, n_substances, scenes, stats);
+            if (r < 0) return r;
+            if (r == RT_OK) {
+                for (int k = 0; k < c->n_dev; k++) c->dev[k].scene = scenes[k];
+                c->scatter = e.scatter;
+                c->has_scene = true;
+                rt_builder_synced(b, c->store, rt_store_epoch(c->store), false);
+                return RT_OK;
+            }
+        }
+    }
+    // full: linearise and upload (the slots are the DFS order the builder records)
+    rt_scene_desc d;
+    int r = rt_builder_desc(b, shades, n_shades, substance_ri, n_substances, &d);
+    if (r != RT_OK) return r;
+    r = upload(c, &d, false, stats);
+    if (r != RT_OK) return r;
+    if (stats) stats->full = 1;
+    rt_builder_synced(b, c->store, rt_store_epoch(c->store), true);
+    return RT_OK;
+}
+
 static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg)
 {
     if (!c || !cam || !cfg) return rt_set_error(RT_E_INVALID, "null argument");

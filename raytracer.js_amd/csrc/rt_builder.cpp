@@ -47,6 +47,16 @@ struct rt_builder {
     std::vector<int32_t> l_parent, l_child, l_begin, l_count, l_list, l_type, l_shade, l_sub;
     std::vector<rt_shade> l_shades;
     std::vector<double> l_ri;
+    std::vector<int> l_order;          // builder node of each DFS id (the last rt_builder_desc)
+    // rt_builder_sync: the store state this builder was last synced with, the device slot of every
+    // node synced then, and the journal of edits since (nodes whose EntitySet or member entities
+    // changed, parents that gained a child, entities whose data changed)
+    const RtSceneStore *sync_store = nullptr;
+    uint64_t sync_epoch = 0;
+    std::vector<int32_t> slot;
+    size_t synced_nodes = 0, synced_ents = 0;
+    std::vector<int> j_nodes, j_child, j_ents;
+    bool j_full = false;               // an edit the journal cannot express (replaced child, outward growth)
 };
 
 using namespace rtjs;
@@ -162,7 +172,9 @@ static int extend_inside(rt_builder *b, int root, int node, const double a[3], d
         int idx = (int)(((uint32_t)xyz[2] << 2) | ((uint32_t)xyz[1] << 1) | ((uint32_t)xyz[0] << 0));
         if (!(idx >= 0 && idx <= 7)) return -1;
         int nt = new_node(b, sp, cs / 2, cur);
+        if (b->nodes[cur].child[idx] >= 0) b->j_full = true;
         b->nodes[cur].child[idx] = nt;          // replaces an existing child, exactly like Octree.set
+        b->j_child.push_back(cur);
         cur = nt;
         cur_depth++;
     }
@@ -172,6 +184,7 @@ static int extend_inside(rt_builder *b, int root, int node, const double a[3], d
 static int extend_outside(rt_builder *b, int root, int node, const double a[3], double asize, int max_depth)
 {
     if (b->nodes[node].parent >= 0) return -1;
+    b->j_full = true;                           // a new root above the synced one
     int cur_depth = get_level(b, root) - get_level(b, node);
     int cur = node;
     while (cur_depth < max_depth) {
@@ -267,6 +280,8 @@ extern "C" int rt_builder_add(rt_builder *b, const rt_entity_in *in, int32_t *en
     e.owner = fit;
     b->ents.push_back(e);
     b->nodes[fit].set.push_back(id);   // a fresh entity: Set.add appends
+    b->j_nodes.push_back(fit);
+    b->j_ents.push_back(id);
     if (entity_id) *entity_id = id;
     return RT_OK;
 }
@@ -300,9 +315,12 @@ extern "C" int rt_builder_move(rt_builder *b, int32_t id, const double pos[3])
     if (m.owner >= 0) {
         std::vector<int> &set = b->nodes[m.owner].set;
         set.erase(std::find(set.begin(), set.end(), id));
+        b->j_nodes.push_back(m.owner);
     }
     m.owner = fit;
     b->nodes[fit].set.push_back(id);
+    b->j_nodes.push_back(fit);
+    b->j_ents.push_back(id);
     return RT_OK;
 }
 
@@ -312,6 +330,8 @@ extern "C" int rt_builder_set_shade(rt_builder *b, int32_t id, int32_t shade, in
     if (id < 0 || id >= (int32_t)b->ents.size()) return rt_set_error(RT_E_INVALID, "rt_builder_set_shade: entity %d", id);
     b->ents[id].shade = shade;
     b->ents[id].substance = substance;
+    if (b->ents[id].owner >= 0) b->j_nodes.push_back(b->ents[id].owner);   // its prim record carries the shade
+    b->j_ents.push_back(id);
     return RT_OK;
 }
 
@@ -344,6 +364,7 @@ extern "C" int rt_builder_desc(rt_builder *b, const rt_shade *shades, int32_t n_
             if (b->nodes[t].child[c] >= 0) stack.push_back(b->nodes[t].child[c]);
     }
     const size_t n = order.size();
+    b->l_order = order;
     b->l_pos.assign(3 * n, 0);
     b->l_size.assign(n, 0);
     b->l_parent.assign(n, -1);
@@ -394,4 +415,118 @@ extern "C" int rt_builder_desc(rt_builder *b, const rt_shade *shades, int32_t n_
     out->shades = b->l_shades.data();
     out->substance_ri = b->l_ri.data();
     return RT_OK;
+}
+
+// ---- rt_builder_sync (rt_api.hip) --------------------------------------------------------------------
+// index_within_parent (src/octree_space.ts:113-125) of node n, as check_node computes it.
+static int32_t octant_in_parent(const rt_builder *b, int n)
+{
+    const int p = b->nodes[n].parent;
+    if (p < 0) return RT_OCT_UNDEF;
+    const double sc = 2 / b->nodes[p].size;
+    const int32_t ix = toint32((b->nodes[n].pos[0] - b->nodes[p].pos[0]) * sc);
+    const int32_t iy = toint32((b->nodes[n].pos[1] - b->nodes[p].pos[1]) * sc);
+    const int32_t iz = toint32((b->nodes[n].pos[2] - b->nodes[p].pos[2]) * sc);
+    const double idx = octant_sum(ix, iy, iz);
+    return (idx >= 0 && idx <= 7) ? (int32_t)idx : RT_OCT_BAD;
+}
+
+static bool rough_mirror(const rt_shade &sh)
+{
+    return !sh.light && sh.response == RT_RESP_REFLECTION && sh.mirror && sh.roughness > 0.0;
+}
+
+int rt_builder_edit(rt_builder *b, const RtSceneStore *st, uint64_t epoch, const rt_shade *shades, int32_t n_shades,
+                    RtEdit &e)
+{
+    if (b->sync_store != st || b->sync_epoch != epoch || b->j_full || b->nodes[b->root].parent >= 0) return 1;
+    const int N = (int)b->nodes.size();
+    const int n_old = (int)b->synced_nodes;
+    // new nodes take the next slots in creation order; every node is reachable (no child was replaced)
+    b->slot.resize(N);
+    for (int n = n_old; n < N; n++) b->slot[n] = n;
+    for (int n = 0; n < N; n++)
+        if (b->slot[n] < 0) return 1;            // a node the last full sync did not reach
+    e = RtEdit{};
+    e.n_slots = N;
+    e.n_entities = (int32_t)b->ents.size();
+    // node records: new nodes and the old parents that gained a child
+    std::vector<int> rec(b->j_child.begin(), b->j_child.end());
+    for (int n = n_old; n < N; n++) rec.push_back(n);
+    std::sort(rec.begin(), rec.end(), [&](int x, int y) { return b->slot[x] < b->slot[y]; });
+    rec.erase(std::unique(rec.begin(), rec.end()), rec.end());
+    for (int n : rec) {
+        const BNode &nd = b->nodes[n];
+        e.rec_slot.push_back(b->slot[n]);
+        for (int i = 0; i < 3; i++) e.rec_cube.push_back(nd.pos[i]);
+        e.rec_cube.push_back(nd.size);
+        for (int c = 0; c < 8; c++) e.rec_child.push_back(nd.child[c] >= 0 ? b->slot[nd.child[c]] : -1);
+        e.rec_up.push_back(n == b->root || nd.parent < 0 ? -1 : b->slot[nd.parent]);
+        e.rec_up.push_back(n == b->root ? RT_OCT_UNDEF : octant_in_parent(b, n));
+    }
+    // dirty EntitySets: journaled nodes and every new node
+    std::vector<int> dirty(b->j_nodes.begin(), b->j_nodes.end());
+    for (int n = n_old; n < N; n++) dirty.push_back(n);
+    std::sort(dirty.begin(), dirty.end(), [&](int x, int y) { return b->slot[x] < b->slot[y]; });
+    dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+    for (int n : dirty) {
+        const std::vector<int> &set = b->nodes[n].set;
+        e.set_slot.push_back(b->slot[n]);
+        e.set_begin.push_back((int32_t)e.set_ent.size());
+        e.set_count.push_back((int32_t)set.size());
+        for (int id : set) {
+            const BEnt &x = b->ents[id];
+            if (x.shade < 0 || x.shade >= n_shades)
+                return rt_set_error(RT_E_INVALID, "rt_builder_sync: entity %d shade %d (%d shades)", id, x.shade, n_shades);
+            e.set_ent.push_back(id);
+            e.set_type.push_back(x.type);
+            e.set_shade.push_back(x.shade);
+            e.set_geom.insert(e.set_geom.end(), x.g, x.g + 9);
+        }
+    }
+    // substances of the edited and the new entities
+    std::vector<int> ents(b->j_ents.begin(), b->j_ents.end());
+    for (size_t i = b->synced_ents; i < b->ents.size(); i++) ents.push_back((int)i);
+    std::sort(ents.begin(), ents.end());
+    ents.erase(std::unique(ents.begin(), ents.end()), ents.end());
+    for (int id : ents) {
+        e.sub_ent.push_back(id);
+        e.sub_val.push_back(b->ents[id].substance);
+    }
+    // DFS numbering (the node ids the outputs report) changes only when nodes were created
+    if (N > n_old) {
+        e.dfs.assign(N, -1);
+        std::vector<int> stack{b->root};
+        int k = 0;
+        while (!stack.empty()) {
+            const int t = stack.back();
+            stack.pop_back();
+            e.dfs[b->slot[t]] = k++;
+            for (int c = 7; c >= 0; c--)
+                if (b->nodes[t].child[c] >= 0) stack.push_back(b->nodes[t].child[c]);
+        }
+    }
+    // a rough mirror is listed: only scenes whose shade table has one pay the entity scan
+    bool any = false;
+    for (int i = 0; i < n_shades; i++) any = any || rough_mirror(shades[i]);
+    for (size_t i = 0; any && !e.scatter && i < b->ents.size(); i++)
+        e.scatter = b->ents[i].owner >= 0 && b->ents[i].shade >= 0 && b->ents[i].shade < n_shades &&
+                    rough_mirror(shades[b->ents[i].shade]);
+    return 0;
+}
+
+void rt_builder_synced(rt_builder *b, const RtSceneStore *st, uint64_t epoch, bool full)
+{
+    if (full) {                                  // a full upload numbers the slots in DFS order
+        b->slot.assign(b->nodes.size(), -1);
+        for (size_t k = 0; k < b->l_order.size(); k++) b->slot[b->l_order[k]] = (int32_t)k;
+    }
+    b->synced_nodes = b->nodes.size();
+    b->synced_ents = b->ents.size();
+    b->j_nodes.clear();
+    b->j_child.clear();
+    b->j_ents.clear();
+    b->j_full = false;
+    b->sync_store = st;
+    b->sync_epoch = epoch;
 }

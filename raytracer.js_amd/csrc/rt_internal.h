@@ -3,6 +3,8 @@
 
 #include <stdint.h>
 
+#include <vector>
+
 #include "rt.h"
 
 // Error reporting: thread-local message behind rt_last_error().
@@ -111,6 +113,38 @@ RtSceneStore *rt_store_new(bool sah, int ndev, const int *devs, void *const *str
 void rt_store_free(RtSceneStore *st);
 int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, RtDevScene *dev, bool *scatter,
                     rt_update_stats *stats);
+// Every upload / update / edit of a store bumps its epoch: a builder's journal is only valid
+// against the store state it was synced with.
+uint64_t rt_store_epoch(const RtSceneStore *st);
+
+// An edit of the resident scene made through the native builder since its last rt_builder_sync
+// (rt_builder.cpp builds it from the builder's journal, rt_scene.hip applies it): O(edit) on the
+// host, no linearisation and no diff of the whole scene.
+struct RtEdit {
+    int32_t n_slots = 0;                   // node slots after the edit (existing slots keep their number)
+    int32_t n_entities = 0;
+    // node records to (re)write: new slots, and existing ones that gained a child; ascending slots
+    std::vector<int32_t> rec_slot;
+    std::vector<double> rec_cube;          // 4 per record: pos.xyz, size
+    std::vector<int32_t> rec_child;        // 8 per record: child slots, -1 empty
+    std::vector<int32_t> rec_up;           // 2 per record: parent slot (-1 root), index_within_parent
+    // nodes whose EntitySet or a member entity changed (and every new node): the set in Set order
+    std::vector<int32_t> set_slot, set_begin, set_count;
+    std::vector<int32_t> set_ent, set_type, set_shade;    // per member
+    std::vector<double> set_geom;                         // 9 per member (rt_scene_desc.ent_geom layout)
+    std::vector<int32_t> sub_ent, sub_val;                // entities whose substance is (re)sent
+    std::vector<int32_t> dfs;              // node_dfs of every slot when the DFS numbering changed, else empty
+    bool scatter = false;                  // a rough mirror is listed
+};
+// 0: `out` holds the edit since the builder's sync with (st, epoch); 1: a full upload is needed
+// (never synced with this store state, or an edit the journal cannot express).
+int rt_builder_edit(rt_builder *b, const RtSceneStore *st, uint64_t epoch, const rt_shade *shades, int32_t n_shades,
+                    RtEdit &out);
+// After a successful sync: `full` = the scene went up through rt_builder_desc + a full upload.
+void rt_builder_synced(rt_builder *b, const RtSceneStore *st, uint64_t epoch, bool full);
+// RT_OK, 1 (a full upload is needed: the pools are mostly garbage), or an error.
+int rt_store_apply_edit(RtSceneStore *st, const RtEdit &e, const rt_shade *shades, int32_t n_shades,
+                        const double *substance_ri, int32_t n_substances, RtDevScene *dev, rt_update_stats *stats);
 
 // Kernel launchers (rt_kernels.hip).
 struct RtLaunch {

@@ -202,13 +202,11 @@ int validate(const rt_scene_desc *s, std::vector<int32_t> &oct, bool &scatter)
     return RT_OK;
 }
 
-// The exact-test record of entity e at Set rank `rank`.
-RtPrim make_rec(const rt_scene_desc *s, int e, int rank)
+// The exact-test record of an entity (type, geometry g[9], shade) at Set rank `rank`.
+RtPrim make_rec_raw(int type, const double *g, int shade, int rank)
 {
-    const double *g = s->ent_geom + 9 * (size_t)e;
     RtPrim p;
     memset(&p, 0, sizeof p);
-    const int type = s->ent_type[e];
     if (type == RT_ENT_SPHERE) {
         p.g[0] = g[0]; p.g[1] = g[1]; p.g[2] = g[2];
         p.g[3] = g[4];            // _dot_pp
@@ -224,9 +222,14 @@ RtPrim make_rec(const rt_scene_desc *s, int e, int rank)
             p.g[6 + i] = g[6 + i] - g[i];   // e2 = v2 - v0
         }
     }
-    p.meta = type | (s->ent_shade[e] << 2);
+    p.meta = type | (shade << 2);
     p.rank = rank;
     return p;
+}
+
+RtPrim make_rec(const rt_scene_desc *s, int e, int rank)
+{
+    return make_rec_raw(s->ent_type[e], s->ent_geom + 9 * (size_t)e, s->ent_shade[e], rank);
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0)
@@ -255,6 +258,11 @@ struct RtSceneStore {
     std::vector<RtImage> m_images;
     std::vector<uint8_t> m_texels;                     // all images' bytes, padded to 4
     size_t list_used = 0, bvh_used = 0;
+    size_t list_live = 0;                              // list-pool entries in use by some EntitySet
+    uint64_t epoch = 0;                                // bumped by every upload, update and edit
+    bool desc_mirrors = false;                         // m_list / m_order / slot_of / entity mirrors match the
+                                                       // device (an rt_builder_sync edit does not keep them)
+    int32_t n_ent = 0, n_shades = 0, n_subs = 0;
     // the scene is replicated on every device of the context: one set of host mirrors, one set of
     // device arrays (and one staging buffer) per device, all written from the same staging bytes
     int ndev = 1;
@@ -406,7 +414,7 @@ struct RtSceneStore {
         return RT_OK;
     }
 
-    void fill(const rt_scene_desc *s, int k, RtDevScene &d) const
+    void fill(int k, RtDevScene &d) const
     {
         const DevArr *a = this->a[k];
         d.node = (const RtNode *)a[A_NODE].p;
@@ -426,9 +434,9 @@ struct RtSceneStore {
         d.n_images = (int32_t)m_images.size();
         d.n_nodes = (int32_t)slots.size();
         d.n_list = (int32_t)list_used;
-        d.n_entities = s->n_entities;
-        d.n_shades = s->n_shades;
-        d.n_subs = s->n_substances;
+        d.n_entities = n_ent;
+        d.n_shades = n_shades;
+        d.n_subs = n_subs;
         d.n_bvh = (int32_t)bvh_used;
     }
 
@@ -539,6 +547,12 @@ struct RtSceneStore {
         us.full = 1;
         us.dirty_nodes = N;
         us.changed_entities = s->n_entities;
+        list_live = (size_t)NL;
+        n_ent = s->n_entities;
+        n_shades = s->n_shades;
+        n_subs = s->n_substances;
+        desc_mirrors = true;
+        epoch++;
         has = true;
         return RT_OK;
     }
@@ -548,7 +562,7 @@ struct RtSceneStore {
     {
         const int N = s->n_nodes, NL = s->n_list, NE = s->n_entities;
         const auto t0 = std::chrono::steady_clock::now();
-        if (!has || node_key(s, 0) != root || NE < (int)m_type.size()) return 1;
+        if (!has || !desc_mirrors || node_key(s, 0) != root || NE < (int)m_type.size()) return 1;
         // 1. node slots.  Old nodes keep their relative DFS order (nodes are only ever inserted), so
         // one merge pass over the old DFS sequence matches them; anything else falls back to the
         // cube -> slot hash.
@@ -601,6 +615,7 @@ struct RtSceneStore {
         slots.resize(n_slots, Slot{0, 0, 0, 0, 0, -1});   // a full upload (return 1) reassigns them
         size_t lu = list_used, bu = bvh_used, dirty_list = 0;
         int moved = 0;
+        size_t live = list_live;
         for (int n = 0; n < N; n++) {
             const int sl = slot_of_dfs[n];
             const int b = s->node_ent_begin[n], c = s->node_ent_count[n];
@@ -611,6 +626,7 @@ struct RtSceneStore {
             if (!d) continue;
             dirty.push_back({n, sl});
             dirty_list += c;
+            live += (size_t)c - (size_t)S.cnt;
             if (c > S.lcap) {
                 moved += sl < (int)n_old;
                 S.lcap = c + c / 2 + 2;
@@ -745,11 +761,140 @@ struct RtSceneStore {
             has = false;                            // the device copy is no longer known
             return r;
         }
+        list_live = live;
+        n_ent = NE;
+        n_shades = s->n_shades;
+        n_subs = s->n_substances;
+        epoch++;
         us.full = 0;
         us.dirty_nodes = (int32_t)dirty.size();
         us.new_nodes = new_nodes;
         us.moved_regions = moved;
         us.changed_entities = n_chg;
+        return RT_OK;
+    }
+
+    // An edit from the native builder's journal (RtEdit, rt_builder.cpp): only the named node records,
+    // EntitySets and entity substances are rebuilt and sent.  Returns 1 when a full upload is needed.
+    int apply_edit(const RtEdit &e, const rt_shade *shades, int ns, const double *ri, int nri, rt_update_stats &us)
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        const size_t n_old = slots.size();
+        if (!has || (size_t)e.n_slots < n_old) return 1;
+        for (size_t k = 0; k < e.sub_ent.size(); k++)
+            if (e.sub_val[k] < -1 || e.sub_val[k] >= nri)
+                return rt_set_error(RT_E_INVALID, "rt_builder_sync: entity %d substance %d", e.sub_ent[k], e.sub_val[k]);
+        // 1. regions of the rebuilt sets (in place when they fit, else at the end of the pools)
+        slots.resize(e.n_slots, Slot{0, 0, 0, 0, 0, -1});
+        size_t lu = list_used, bu = bvh_used, live = list_live;
+        int moved = 0;
+        for (size_t k = 0; k < e.set_slot.size(); k++) {
+            Slot &S = slots[e.set_slot[k]];
+            const int c = e.set_count[k];
+            live += (size_t)c - (size_t)S.cnt;
+            if (c > S.lcap) {
+                moved += e.set_slot[k] < (int32_t)n_old;
+                S.lcap = c + c / 2 + 2;
+                S.lbeg = (int32_t)lu;
+                lu += S.lcap;
+                S.bcap = 2 * S.lcap - 1;
+                S.bbeg = (int32_t)bu;
+                bu += S.bcap;
+            }
+            S.cnt = c;
+        }
+        if (lu > 2 * live + 65536) return 1;           // the pools are mostly garbage: compact
+        list_used = lu;
+        bvh_used = bu;
+        list_live = live;
+        const size_t NS = (size_t)e.n_slots;
+        int r = reserve_all(NS, (size_t)e.n_entities, (size_t)ns, (size_t)nri, m_images.size(), m_texels.size(), true);
+        if (r != RT_OK) return r;
+        m_node.resize(NS);
+        m_up.resize(2 * NS, 0);
+        m_ent.resize(4 * NS, 0);
+        m_dfs.resize(NS, 0);
+        // 2. the rebuilt sets: prim records in cull order, hierarchy, Set-order ids, prefix, within
+        std::vector<RtPrim> recs, prim;
+        std::vector<RtBvh> bvh;
+        std::vector<int32_t> prefix, wslots;
+        for (size_t k = 0; k < e.set_slot.size(); k++) {
+            const int sl = e.set_slot[k], c = e.set_count[k], b0 = e.set_begin[k];
+            Slot &S = slots[sl];
+            recs.resize(c);
+            prim.resize(c);
+            bvh.resize(c ? 2 * (size_t)c - 1 : 0);
+            prefix.resize(4 * (size_t)c);
+            for (int i = 0; i < c; i++)
+                recs[i] = make_rec_raw(e.set_type[b0 + i], &e.set_geom[9 * (size_t)(b0 + i)], e.set_shade[b0 + i], S.lbeg + i);
+            S.broot = c ? rt_build_node_cull(recs.data(), c, S.lbeg, S.bbeg, delta, clampv, sah, prim.data(), bvh.data(),
+                                             prefix.data())
+                        : -1;
+            add(A_PRIM, sizeof(RtPrim) * (size_t)S.lbeg, prim.data(), sizeof(RtPrim) * (size_t)c);
+            add(A_BVH, sizeof(RtBvh) * (size_t)S.bbeg, bvh.data(), sizeof(RtBvh) * bvh.size());
+            add(A_LIST, 4 * (size_t)S.lbeg, &e.set_ent[b0], 4 * (size_t)c);
+            add(A_PREFIX, 16 * (size_t)S.lbeg, prefix.data(), 16 * (size_t)c);
+            wslots.resize((size_t)std::max(c, 1));
+            const int wc = c ? within_slots(prim.data(), c, S.lbeg, wslots.data()) : 0;
+            add(A_WITHIN, 4 * (size_t)S.lbeg, wslots.data(), 4 * (size_t)wc);
+            m_ent[4 * (size_t)sl] = S.lbeg;
+            m_ent[4 * (size_t)sl + 1] = c;
+            m_ent[4 * (size_t)sl + 2] = S.broot;
+            m_ent[4 * (size_t)sl + 3] = wc;
+            m_node[sl].n_ent = c;
+            m_node[sl].ent_begin = S.lbeg;
+            m_node[sl].bvh_root = S.broot;
+            m_node[sl].box = c ? bvh[0] : RtBvh{};
+        }
+        // 3. node records: cube, children, parent link
+        for (size_t k = 0; k < e.rec_slot.size(); k++) {
+            const int sl = e.rec_slot[k];
+            RtNode &nd = m_node[sl];
+            nd.x = e.rec_cube[4 * k]; nd.y = e.rec_cube[4 * k + 1]; nd.z = e.rec_cube[4 * k + 2]; nd.s = e.rec_cube[4 * k + 3];
+            for (int c = 0; c < 8; c++) nd.child[c] = e.rec_child[8 * k + c];
+            nd.up_tree = m_up[2 * (size_t)sl] = e.rec_up[2 * k];
+            nd.up_oct = m_up[2 * (size_t)sl + 1] = e.rec_up[2 * k + 1];
+        }
+        add_slots(A_NODE_UP, e.rec_slot, m_up.data(), 2 * sizeof(int32_t));
+        std::vector<int32_t> ent_slots(e.set_slot);
+        std::sort(ent_slots.begin(), ent_slots.end());
+        add_slots(A_NODE_ENT, ent_slots, m_ent.data(), 4 * sizeof(int32_t));
+        std::vector<int32_t> rec_slots(e.rec_slot);
+        rec_slots.insert(rec_slots.end(), ent_slots.begin(), ent_slots.end());
+        std::sort(rec_slots.begin(), rec_slots.end());
+        rec_slots.erase(std::unique(rec_slots.begin(), rec_slots.end()), rec_slots.end());
+        add_slots(A_NODE, rec_slots, m_node.data(), sizeof(RtNode));
+        // 4. entity substances (runs of consecutive ids), DFS ids, tables
+        for (size_t i = 0; i < e.sub_ent.size();) {
+            size_t j = i + 1;
+            while (j < e.sub_ent.size() && e.sub_ent[j] == e.sub_ent[j - 1] + 1) j++;
+            add(A_ENT_SUB, 4 * (size_t)e.sub_ent[i], &e.sub_val[i], 4 * (j - i));
+            i = j;
+        }
+        if (!e.dfs.empty()) diff_runs(A_NODE_DFS, e.dfs, m_dfs, 1);
+        if (m_shades.size() != (size_t)ns || (ns && memcmp(m_shades.data(), shades, sizeof(rt_shade) * ns) != 0)) {
+            m_shades.assign(shades, shades + ns);
+            add(A_SHADES, 0, m_shades.data(), sizeof(rt_shade) * m_shades.size());
+        }
+        if (m_ri.size() != (size_t)nri || (nri && memcmp(m_ri.data(), ri, 8 * (size_t)nri) != 0)) {
+            m_ri.assign(ri, ri + nri);
+            add(A_SUB_RI, 0, m_ri.data(), 8 * m_ri.size());
+        }
+        us.host_ms = ms_since(t0);
+        if ((r = flush(&us.bytes)) != RT_OK) {
+            has = false;
+            return r;
+        }
+        desc_mirrors = false;                       // a later rt_update_scene re-uploads in full
+        n_ent = e.n_entities;
+        n_shades = ns;
+        n_subs = nri;
+        epoch++;
+        us.full = 0;
+        us.dirty_nodes = (int32_t)e.set_slot.size();
+        us.new_nodes = (int32_t)(NS - n_old);
+        us.moved_regions = moved;
+        us.changed_entities = (int32_t)e.sub_ent.size();
         return RT_OK;
     }
 };
@@ -796,8 +941,28 @@ int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, 
         if (r != RT_OK) return r;
     }
     us.host_ms += validate_ms;
-    for (int k = 0; k < st->ndev; k++) st->fill(s, k, dev[k]);
+    for (int k = 0; k < st->ndev; k++) st->fill(k, dev[k]);
     *scatter = sc;
+    us.total_ms = ms_since(t0);
+    if (stats) *stats = us;
+    return RT_OK;
+}
+
+uint64_t rt_store_epoch(const RtSceneStore *st) { return st->epoch; }
+
+int rt_store_apply_edit(RtSceneStore *st, const RtEdit &e, const rt_shade *shades, int32_t n_shades,
+                        const double *substance_ri, int32_t n_substances, RtDevScene *dev, rt_update_stats *stats)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    rt_update_stats us;
+    memset(&us, 0, sizeof us);
+    for (int k = 0; k < st->ndev; k++) {            // no frame may read the scene while it changes
+        HIP_TRY(hipSetDevice(st->devs[k]));
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    const int r = st->apply_edit(e, shades, n_shades, substance_ri, n_substances, us);
+    if (r != RT_OK) return r;
+    for (int k = 0; k < st->ndev; k++) st->fill(k, dev[k]);
     us.total_ms = ms_since(t0);
     if (stats) *stats = us;
     return RT_OK;

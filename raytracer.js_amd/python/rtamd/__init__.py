@@ -244,6 +244,16 @@ class Context:
         self.scene = scene
         _check(self.L.rt_upload_scene(self.h, C.byref(scene.desc())))
 
+    def sync(self, builder):
+        """rt_builder_sync: make the resident scene the builder's tree, sending only what its edits
+        since the last sync changed; returns rt_update_stats."""
+        self.scene = None
+        st = abi.rt_update_stats()
+        _check(self.L.rt_builder_sync(self.h, builder.h, builder.shades.ctypes.data_as(C.POINTER(abi.rt_shade)),
+                                      len(builder.shades), builder.substances.ctypes.data_as(C.POINTER(C.c_double)),
+                                      len(builder.substances), C.byref(st)))
+        return st
+
     def update(self, scene):
         """rt_update_scene: incremental re-upload of an edited scene; returns rt_update_stats."""
         self.scene = scene

@@ -129,7 +129,7 @@ EXPORTS = ("rt_create", "rt_destroy", "rt_last_error", "rt_abi_version", "rt_upl
            "rt_debug_camera_dirs", "rt_builder_create", "rt_builder_destroy", "rt_builder_add",
            "rt_builder_add_many", "rt_builder_desc", "rt_exposure_stats_device", "rt_tonemap_device",
            "rt_tonemap_range", "rt_update_scene", "rt_builder_move", "rt_builder_set_shade",
-           "rt_trace_frame_device", "rt_frame_fault", "rt_ctx_info_get")
+           "rt_trace_frame_device", "rt_frame_fault", "rt_ctx_info_get", "rt_builder_sync")
 
 
 def declare(lib):
@@ -159,6 +159,7 @@ def declare(lib):
     lib.rt_tonemap_device.argtypes = [vp, vp, C.c_int64, _d, _d, vp, vp]
     lib.rt_tonemap_range.argtypes = [_i, P(rt_exposure_stats), _i, _d, _d, _pd]
     lib.rt_update_scene.argtypes = [vp, P(rt_scene_desc), P(rt_update_stats)]
+    lib.rt_builder_sync.argtypes = [vp, vp, P(rt_shade), _i, _pd, _i, P(rt_update_stats)]
     lib.rt_builder_move.argtypes = [vp, _i, _pd]
     lib.rt_builder_set_shade.argtypes = [vp, _i, _i, _i]
     lib.rt_trace_frame_device.argtypes = [vp, P(rt_camera_desc), P(rt_config_desc), vp, vp]

@@ -237,3 +237,85 @@ def test_update_shade_table_and_scatter_gate():
             fresh.close()
     finally:
         ctx.close()
+
+
+# ---- rt_builder_sync: O(edit) re-upload from the builder's journal ---------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 4])
+def test_builder_sync_equals_full_upload_and_oracle(seed):
+    """rt_builder_sync after each edit of the script: only the edit's nodes travel (no linearisation,
+    no diff of the whole scene), and the frame equals a fresh rt_upload_scene of the builder's
+    linearised tree and, periodically, the oracle's frame."""
+    spec = scenes.small_random(seed, n_tri=600)
+    cam, cfg = scenes.make_camera(160, 120), scenes.make_config(3)
+    p = Pair(spec)
+    ctx, fresh = rtamd.Context(0), rtamd.Context(0)
+    try:
+        st = ctx.sync(p.b)
+        assert st.full == 1                                   # the first sync uploads in full
+        for i, op in enumerate(_edits(spec, seed)):
+            p.apply(op)
+            st = ctx.sync(p.b)
+            assert st.full == 0, st.as_dict()
+            assert st.dirty_nodes <= 4 and st.bytes < 64 * 1024, st.as_dict()
+            got = _frame(ctx, cam, cfg)
+            fresh.upload(p.b.arrays())
+            _same(got, _frame(fresh, cam, cfg))
+            if i % 4 == 3:
+                _same(got, p.w.trace_frame(p.root, cam, cfg, nthreads=8))
+    finally:
+        ctx.close()
+        fresh.close()
+        p.close()
+
+
+@pytest.mark.gpu
+def test_builder_sync_new_nodes_shades_and_fallbacks():
+    """Growth into new deeper nodes (appended slots, node_dfs renumbered), shade-table edits that arm the
+    rough-mirror gate, an rt_upload_scene in between (the next sync is full again), and the debug
+    walk's DFS ids."""
+    spec = scenes.config1_spheres()
+    cam, cfg = scenes.make_camera(128, 96), scenes.make_config(4)
+    p = Pair(spec)
+    w, root = p.w, p.root
+    ctx = rtamd.Context(0)
+    try:
+        assert ctx.sync(p.b).full == 1
+        sts = []
+        for k in range(40):
+            c = (0.05 + 0.9 * ((k * 0.381966) % 1), 0.1 + 0.02 * (k % 7), 0.3 + 0.01 * k)
+            p.apply(("add", _entity(abi.RT_ENT_SPHERE, [*c, 0.004], k % 8, depth=7 if k % 3 else 2)))
+            if k % 5 == 4:
+                p.apply(("move", k, (0.2 + 0.015 * k, 0.6, 0.4)), ("shade", k + 1, (k + 3) % 8, 1))
+            sts.append(ctx.sync(p.b).as_dict())
+        assert all(s["full"] == 0 for s in sts)
+        assert sum(s["new_nodes"] for s in sts) > 0 and sum(s["moved_regions"] for s in sts) > 0
+        got = _frame(ctx, cam, cfg)
+        _same(got, w.trace_frame(root, cam, cfg, nthreads=8))
+        w.linearize(root)
+        wk = w.walker(root, include_undefined=True)
+        rng = np.random.default_rng(5)
+        for _ in range(40):
+            o, d = rng.uniform(0.0, 1.0, 3).tolist(), rng.normal(size=3).tolist()
+            ref = [(w.tree_id(pt), -1 if po is None else po) for _, pt, po in w.walk(wk, o, d)]
+            assert ctx.debug_walk(o, d, include_undefined=True) == ref
+        # a rough mirror in the shade table: the gate follows it without a full upload
+        p.b.shades = p.b.shades.copy()
+        p.b.shades["roughness"][1] = 0.4
+        st = ctx.sync(p.b)
+        assert st.full == 0 and st.dirty_nodes == 0
+        with pytest.raises(rtamd.RtError):
+            ctx.trace_frame(cam, cfg)
+        # another upload to the context: the builder's journal no longer applies
+        ctx.upload(rtamd.build_scene(scenes.small_random(2)))
+        assert ctx.sync(p.b).full == 1
+        fresh = rtamd.Context(0)
+        try:
+            fresh.upload(p.b.arrays())
+            cfg_c = scenes.make_config(4, scatter_seed=3)
+            _same(_frame(ctx, cam, cfg_c), _frame(fresh, cam, cfg_c))
+        finally:
+            fresh.close()
+    finally:
+        ctx.close()
+        p.close()

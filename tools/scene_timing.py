@@ -1,8 +1,9 @@
 """Scene build / upload / incremental-update timing.
 
 For each size: native build (rt_builder_add_many), linearisation (rt_builder_desc), full upload
-(rt_upload_scene: validation, per-node cull hierarchies, H2D) and rt_update_scene after moving k
-random entities (Entity._set_pos + add_entity_to_octree).  One JSON line per measurement.
+(rt_upload_scene: validation, per-node cull hierarchies, H2D) and, after moving k random entities
+(Entity._set_pos + add_entity_to_octree), both re-upload paths: rt_builder_desc + rt_update_scene
+(O(scene) on the host) and rt_builder_sync (O(edit)).  One JSON line per measurement.
 
 python tools/scene_timing.py [--tris N ...] [--moves K ...] [--no-gpu]
 """
@@ -48,19 +49,27 @@ def main():
             row["upload_s"] = min(ts)
         print(json.dumps(row), flush=True)
         ne = len(spec.entities) - 1
-        for k in a.moves:
-            ids = rng.choice(ne, k, replace=False)
-            t3 = time.perf_counter()
-            for e in ids:
-                b.move(int(e), rng.uniform(0.05, 0.95, 3))
-            t4 = time.perf_counter()
-            sc = b.arrays()
-            t5 = time.perf_counter()
-            row = dict(tris=n, moves=k, move_s=t4 - t3, desc_s=t5 - t4)
-            if ctx is not None:
-                st = ctx.update(sc)
-                row.update(update_s=time.perf_counter() - t5, **{"st_" + x: v for x, v in st.as_dict().items()})
-            print(json.dumps(row), flush=True)
+        for path in ("update", "sync"):
+            if ctx is not None and path == "sync":
+                st = ctx.sync(b)                                   # first sync: full
+            for k in a.moves:
+                ids = rng.choice(ne, k, replace=False)
+                t3 = time.perf_counter()
+                for e in ids:
+                    b.move(int(e), rng.uniform(0.05, 0.95, 3))
+                t4 = time.perf_counter()
+                row = dict(tris=n, path=path, moves=k, move_s=t4 - t3)
+                if path == "update":
+                    sc = b.arrays()
+                    t5 = time.perf_counter()
+                    row["desc_s"] = t5 - t4
+                    if ctx is not None:
+                        st = ctx.update(sc)
+                        row.update(update_s=time.perf_counter() - t5, **{"st_" + x: v for x, v in st.as_dict().items()})
+                elif ctx is not None:
+                    st = ctx.sync(b)
+                    row.update(sync_s=time.perf_counter() - t4, **{"st_" + x: v for x, v in st.as_dict().items()})
+                print(json.dumps(row), flush=True)
         b.close()
 
 
