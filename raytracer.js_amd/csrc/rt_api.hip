@@ -84,6 +84,7 @@ struct RtDevice {
     std::vector<std::array<hipEvent_t, 2>> ev;   // trace-kernel timing ring
     int ev_next = 0, ev_count = 0;
     hipEvent_t sync = nullptr;                   // cross-stream / cross-device ordering
+    int32_t *h_ctr = nullptr;                    // pinned: the work counters of a recent frame (grid hints)
 };
 
 }  // namespace
@@ -101,6 +102,7 @@ struct rt_ctx {
                                      // their passes are latency-bound, fewer lanes per wave shorten the
                                      // slowest wave
     int seg = 8;                     // segments per bounce ray, levels >= 1 (RT_SEG: 0/1 off, 2..64)
+    int lv_blocks = 0;               // grid cap of bounce-level passes (RT_LV_BLOCKS; 0: persistent occupancy)
     int occ = 0;
     int diag = 0;
     bool has_scene = false;
@@ -174,6 +176,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_SPLIT_LEVELS")) c->split_levels = atoi(e) < 1 ? 1 : atoi(e);
     if (const char *e = getenv("RT_CONT_GROUP")) c->cont_group = pow2_at_most_64(atoi(e));
     if (const char *e = getenv("RT_SEG")) c->seg = atoi(e) > 1 ? pow2_at_most_64(atoi(e)) : 0;
+    if (const char *e = getenv("RT_LV_BLOCKS")) c->lv_blocks = atoi(e) < 0 ? 0 : atoi(e);
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
@@ -260,6 +263,7 @@ extern "C" void rt_destroy(rt_ctx *c)
             for (hipEvent_t x : e)
                 if (x) (void)hipEventDestroy(x);
         if (d.sync) (void)hipEventDestroy(d.sync);
+        if (d.h_ctr) (void)hipHostFree(d.h_ctr);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
     delete c;
@@ -392,6 +396,10 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.fault = (int32_t *)d.b_fault.p;
     L.cull = (c->flags & RT_CREATE_NO_CULL) ? 0 : 1;
     L.ctr = (int32_t *)d.b_ctr.p;
+    if (!d.h_ctr && hipHostMalloc((void **)&d.h_ctr, sizeof(int32_t) * RT_CTR_INTS, hipHostMallocDefault) == hipSuccess)
+        for (int i = 0; i < RT_CTR_INTS; i++) d.h_ctr[i] = -1;        // unknown until a frame completes
+    (void)hipGetLastError();
+    L.ctr_hint = d.h_ctr;
     L.occ = c->occ;
     L.diag = c->diag;
     L.cont_group = c->cont_group;
@@ -400,6 +408,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.xcd_mask = c->xcd_mask;
     L.shade_occ = c->shade_occ;
     L.seg = c->seg;
+    L.lv_blocks = c->lv_blocks;
     L.blend = cfg->col_weight != 1.0;
     if (c->split && P > 0) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot

@@ -180,6 +180,8 @@ struct RtLaunch {
     int32_t shade_occ;                          // k_shade waves per SIMD the registers must admit (3, 4, 5)
     int32_t seg;                                // segments per bounce ray, levels >= 1 (0: off; RT_SEG; §5.10)
     int32_t *ray_cn;                            // device [rows*W]: per-ray status of a segmented level
+    int32_t lv_blocks;                          // grid cap of the bounce-level passes and k_cont (0: full; RT_LV_BLOCKS)
+    int32_t *ctr_hint;                          // pinned host copy of a recent frame's ctr (-1: none yet), or null
 };
 
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };

@@ -1629,7 +1629,7 @@ __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, doub
 // makes an over-estimate harmless (late blocks find the queue empty).  The CU count and each
 // kernel's blocks per CU are queried once (all devices of a context are MI355X): one host thread
 // issues the launches of up to 8 GPUs, so a launch is only the launch.
-static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const RtLaunch &L)
+static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const RtLaunch &L, int max_blocks = 0)
 {
     static std::atomic<int> cus{0};
     static std::mutex mu;
@@ -1652,7 +1652,24 @@ static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const Rt
             per_kernel.emplace_back(kp, per);
         }
     }
-    hipLaunchKernelGGL(kernel, dim3(n_cu * per), dim3(256), 0, st, L);
+    int nb = n_cu * per;
+    if (max_blocks > 0 && nb > max_blocks) nb = max_blocks;
+    hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), 0, st, L);
+}
+
+// Grid of a bounce-level pass (or k_cont).  Persistent passes are correct at any grid size: waves
+// claim work until the level's queue is empty.  A level of a small part holds a few thousand rays,
+// and launching the full persistent grid for it costs more in block dispatch than the work (8-part
+// probe: 516 -> 564 Mrays/s per GPU with 256 blocks).  The grid is sized from the ray count this
+// level had in a recent frame on this context (L.ctr_hint, copied back asynchronously; -1 before
+// the first one completes: the full grid): up to 8 lanes per ray, 2x headroom, at least 256 blocks
+// so that a level that grew since keeps a quarter of the chip.  RT_LV_BLOCKS > 0 forces a cap.
+static int level_blocks(const RtLaunch &L, int32_t hint_rays)
+{
+    if (L.lv_blocks > 0) return L.lv_blocks;
+    if (hint_rays < 0) return 0;
+    const long long est = ((long long)hint_rays * 8 * 2 + 255) / 256;
+    return (int)std::min<long long>(std::max<long long>(256, est), 1 << 20);
 }
 
 int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end)
@@ -1690,16 +1707,19 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             RtLaunch Lv = L;
             Lv.level = lv;
             Lv.last_level = lv == levels && levels < want;
-            launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lv);
+            const int mb = lv >= 1 ? level_blocks(L, L.ctr_hint ? L.ctr_hint[4 + RT_CTR_LEVEL * (lv - 1)] : -1) : 0;
+            launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
-            if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lv);     // one of the two runs (§5.10)
-            launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv);
+            if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lv, mb);     // one of the two runs (§5.10)
+            launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
-            if (lv >= 1 && L.seg > 1) launch_persistent(k_first_seg<4>, st, Lv);
-            launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv);
+            if (lv >= 1 && L.seg > 1) launch_persistent(k_first_seg<4>, st, Lv, mb);
+            launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
         }
-        launch_persistent(k_cont<3>, st, L);
+        launch_persistent(k_cont<3>, st, L, level_blocks(L, L.ctr_hint ? L.ctr_hint[0] : -1));
+        // this frame's counters come back for the next frames' grid hints (any recent frame will do)
+        if (L.ctr_hint) HIP_TRY(hipMemcpyAsync(L.ctr_hint, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipGetLastError());
     if (ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
