@@ -181,6 +181,8 @@ struct RtLaunch {
     int32_t seg;                                // segments per bounce ray, levels >= 1 (0: off; RT_SEG; §5.10)
     int32_t *ray_cn;                            // device [rows*W]: per-ray status of a segmented level
     int32_t lv_blocks;                          // grid cap of the bounce-level passes and k_cont (0: full; RT_LV_BLOCKS)
+    int32_t refill;                             // wide bounce levels: idle lanes that take new rays (0: off; RT_REFILL)
+    int32_t refill_always;                      // refill every wide level, not only where a recent frame had one (tests)
     int32_t *ctr_hint;                          // pinned host copy of a recent frame's ctr (-1: none yet), or null
 };
 

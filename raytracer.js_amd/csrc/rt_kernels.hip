@@ -387,12 +387,12 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
 // same move block the F_AHEAD lanes run.  Lanes in different phases of their walks therefore no
 // longer pay for two copies of the move and two cube loads per trip.  The slot's
 // parent link is read with its child id (one line), so a step_back does not wait for a load.
+// One trip of walker_run for this lane: nothing unless res == 1 (walking); sets res to the walk's end.
 template <bool STOP, bool ALL_FAST, typename Emit>
-__device__ __forceinline__ int walker_run_t(const RtDevScene &S, Walker &w, Emit &&emit, int stop)
+__device__ __forceinline__ void walker_trip(const RtDevScene &S, Walker &w, Emit &&emit, int stop, int &res)
 {
     enum : int { A_NONE = 0, A_STEPIN = 1, A_EXIT = 2, A_MOVE = 3 };
-    int res = w.cur_tree >= 0 ? 1 : 0;
-    for (;;) {
+    {
         int act = A_NONE, lnode = -1;
         int2 up = make_int2(-1, RT_OCT_UNDEF);
         if (res == 1) {
@@ -460,8 +460,16 @@ __device__ __forceinline__ int walker_run_t(const RtDevScene &S, Walker &w, Emit
                 }
             }
         }
-        if (!__ballot(res == 1)) break;
     }
+}
+
+template <bool STOP, bool ALL_FAST, typename Emit>
+__device__ __forceinline__ int walker_run_t(const RtDevScene &S, Walker &w, Emit &&emit, int stop)
+{
+    int res = w.cur_tree >= 0 ? 1 : 0;
+    do {
+        walker_trip<STOP, ALL_FAST>(S, w, emit, stop, res);
+    } while (__ballot(res == 1));
     return res;
 }
 
@@ -1436,6 +1444,73 @@ __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
     }
 }
 
+// Walk pass of a wide bounce level with per-lane refill (RT_REFILL = G > 0; levels of 64 rays per
+// wave that run unsegmented, config 5's millions of mirror / glass rays).  Such rays are incoherent
+// and their walks differ in length, so a wave of 64 of them idles most lanes long before its
+// slowest ray ends.  Here a lane whose walk ended writes its cand_n and, once G lanes of the wave
+// are idle, they take the next rays of the level's queue with one atomic.  Each ray's walk is the
+// same sequence of operations, so the lists are identical.
+__device__ __forceinline__ bool refill_level(const RtLaunch &L)
+{
+    return L.refill > 0 && L.level >= 1 && !seg_mode(L) && cont_g(L) == 64;
+}
+
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
+{
+    if (!refill_level(L)) return;
+    constexpr int IDLE = 9;
+    const int lane = threadIdx.x & 63;
+    const RtDevScene &S = L.scene;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    const int n_rays = *lvl_ctr(L, L.level - 1);
+    int32_t *head = pass_heads(L, L.level, 1);
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Walker w;
+    RayBox rb;
+    int q = 0, n = 0, res = IDLE;           // res: 1 walking, IDLE without a ray, else the walk's end
+    bool drained = false;
+    const unsigned long long below = (1ull << lane) - 1;
+    for (;;) {
+        const unsigned long long m_walk = __ballot(res == 1);
+        const int idle = 64 - __popcll(m_walk);
+        if (!drained && (idle >= L.refill || !m_walk)) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(head, idle);
+            base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+            drained = base + idle >= n_rays;
+            const int r = base + __popcll(~m_walk & below);
+            if (res != 1 && r < n_rays) {
+                q = r;
+                n = 0;
+                const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
+                const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
+                rb = make_raybox(o, d);
+                if (walker_set(S, w, o, d, false, 0, 0, c) < 0) L.cand_n[q] = 3;
+                else if (w.cur_tree >= 0) res = 1;
+                else L.cand_n[q] = 0;
+            }
+        }
+        if (!__ballot(res == 1)) {
+            if (drained) break;
+            continue;
+        }
+        auto emit = [&](int node) {
+            const RtNode &nd = S.node[node];
+            if (nd.n_ent == 0) return;
+            if (L.cull && rb.ok && !ray_box(nd.box, rb)) return;
+            if (n < L.cand_cap) L.cand[(size_t)n * stride + q] = node;
+            n++;
+        };
+        walker_trip<false, false>(S, w, emit, -1, res);
+        if (res != 1 && res != IDLE) {
+            const int end = res == 0 ? 0 : (res == -2 ? 2 : 1);
+            L.cand_n[q] = n > L.cand_cap ? -1 : n * 4 + end;
+            res = IDLE;
+        }
+    }
+}
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
 {
@@ -1445,7 +1520,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (seg_mode(L)) return;                          // k_walk_seg takes this level
+    if (seg_mode(L) || refill_level(L)) return;       // k_walk_seg / k_walk_refill take this level
     for (;;) {
         int t_end;
         const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
@@ -1707,10 +1782,14 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             RtLaunch Lv = L;
             Lv.level = lv;
             Lv.last_level = lv == levels && levels < want;
-            const int mb = lv >= 1 ? level_blocks(L, L.ctr_hint ? L.ctr_hint[4 + RT_CTR_LEVEL * (lv - 1)] : -1) : 0;
+            const int32_t hint = lv >= 1 && L.ctr_hint ? L.ctr_hint[4 + RT_CTR_LEVEL * (lv - 1)] : -1;
+            const int mb = lv >= 1 ? level_blocks(L, hint) : 0;
+            // per-lane refill only where a recent frame had a wide level (both walk kernels read Lv.refill)
+            Lv.refill = L.refill_always || hint > 64 * 4096 ? L.refill : 0;
             launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
             if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lv, mb);     // one of the two runs (§5.10)
+            if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<4>, st, Lv, mb);
             launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
             if (lv >= 1 && L.seg > 1) launch_persistent(k_first_seg<4>, st, Lv, mb);

@@ -325,6 +325,37 @@ def test_continuation_rays_per_wave(ctx, group, monkeypatch):
     _compare(w.trace_frame(root, cam, cfg, nthreads=8), got)
 
 
+@pytest.mark.parametrize("name,refill,cap", [("config1", "1", None), ("small8", "16", None), ("small8", "48", "2"),
+                                              ("transmission", "8", None), ("transmission", "64", "2"),
+                                              ("config2", "16", None)])
+def test_walk_refill_equals_waves(ctx, name, refill, cap, monkeypatch):
+    """Wide bounce levels walked with per-lane refill (RT_REFILL: idle lanes take the next rays of the
+    level) change which lane walks which ray, not the walks: identical frames against whole waves
+    (RT_REFILL=0) and the oracle at refmax 5.  RT_CONT_GROUP=64 and RT_SEG=0 make every bounce level
+    a refill level (RT_REFILL_ALWAYS=1), also when candidate lists overflow (RT_CAND_CAP=2)."""
+    spec = {"config1": scenes.config1_spheres, "small8": lambda: scenes.small_random(8, n_tri=800, half=0.04),
+            "transmission": _transmission_spec, "config2": scenes.config2}[name]()
+    cam, cfg = scenes.make_camera(203, 133), scenes.make_config(5)      # edge tiles with missing pixels
+    scene = rtamd.build_scene(spec)
+    monkeypatch.setenv("RT_SEG", "0")
+    monkeypatch.setenv("RT_CONT_GROUP", "64")
+    monkeypatch.setenv("RT_REFILL_ALWAYS", "1")     # production refills only levels a recent frame showed wide
+    if cap:
+        monkeypatch.setenv("RT_CAND_CAP", cap)
+    frames = []
+    for g in ("0", refill):
+        monkeypatch.setenv("RT_REFILL", g)
+        c = rtamd.Context(0)
+        try:
+            c.upload(scene)
+            frames.append(c.trace_frame(cam, cfg, stats=False, allow_fault=True))
+        finally:
+            c.close()
+    _same_frames(frames[0], frames[1])
+    w, root = oracle.build_scene(spec)
+    _compare(w.trace_frame(root, cam, cfg, nthreads=8), frames[1])
+
+
 def _transmission_spec():
     spec = scenes.small_random(5)
     sh = spec.shades.copy()
@@ -456,3 +487,17 @@ def test_baseline_config5_tiles_and_samples(ctx):
     assert np.all((got["hit_entity"] >= -1) & (got["hit_entity"] < len(spec.entities)))
     assert st.segments > st.primary * 1.02                   # glass + mirrors: multi-bounce paths
     assert ref["counters"]["segments"] > len(pix) * 1.02
+
+
+@pytest.mark.timeout(300)
+def test_hinted_level_grids_and_refill_config5(ctx):
+    """The production schedule of a second frame: bounce-level grids sized from the first frame's
+    ray counts and per-lane refill on its wide levels (config 5's levels hold millions of rays).
+    The second and third frames equal the first, which ran with full grids and no refill, bit for bit
+    on the full 3840x2160 frame."""
+    factory, W, H, refmax = scenes.WORKLOADS["config5"]
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
+    ctx.upload(rtamd.build_scene(factory()))
+    first = ctx.trace_frame(cam, cfg, stats=False, allow_fault=True)
+    for _ in range(2):
+        _same_frames(first, ctx.trace_frame(cam, cfg, stats=False, allow_fault=True))
