@@ -105,6 +105,7 @@ struct rt_ctx {
     int lv_blocks = 0;               // grid cap of bounce-level passes (RT_LV_BLOCKS; 0: persistent occupancy)
     int refill = 16;                 // wide bounce levels walked with per-lane refill (RT_REFILL; 0: off)
     bool refill_always = false;      // RT_REFILL_ALWAYS=1: also levels no recent frame showed wide (tests)
+    int seg_max = 64 * 4096;         // bounce levels of more rays run unsegmented, refilled (RT_SEG_MAX; 0: no limit)
     int occ = 0;
     int diag = 0;
     bool has_scene = false;
@@ -181,6 +182,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_LV_BLOCKS")) c->lv_blocks = atoi(e) < 0 ? 0 : atoi(e);
     if (const char *e = getenv("RT_REFILL")) c->refill = atoi(e) < 0 ? 0 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_REFILL_ALWAYS")) c->refill_always = atoi(e) != 0;
+    if (const char *e = getenv("RT_SEG_MAX")) c->seg_max = atoi(e) < 0 ? 0 : atoi(e);
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
@@ -415,6 +417,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.lv_blocks = c->lv_blocks;
     L.refill = c->refill;
     L.refill_always = c->refill_always;
+    L.seg_max = c->seg_max;
     L.blend = cfg->col_weight != 1.0;
     if (c->split && P > 0) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot

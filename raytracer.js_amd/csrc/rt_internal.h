@@ -183,6 +183,7 @@ struct RtLaunch {
     int32_t lv_blocks;                          // grid cap of the bounce-level passes and k_cont (0: full; RT_LV_BLOCKS)
     int32_t refill;                             // wide bounce levels: idle lanes that take new rays (0: off; RT_REFILL)
     int32_t refill_always;                      // refill every wide level, not only where a recent frame had one (tests)
+    int32_t seg_max;                            // bounce levels of more rays run unsegmented (0: no limit; RT_SEG_MAX)
     int32_t *ctr_hint;                          // pinned host copy of a recent frame's ctr (-1: none yet), or null
 };
 

@@ -1304,8 +1304,9 @@ enum : int { SEG_FIN = 0, SEG_THROW = 1, SEG_CAP = 2, SEG_SEATTHROW = 3, SEG_REA
 
 __device__ __forceinline__ bool seg_mode(const RtLaunch &L)
 {
-    return L.seg > 1 && L.level >= 1 &&
-           (long long)*lvl_ctr(L, L.level - 1) * L.seg <= (long long)L.rows * (long long)L.cam.width;
+    const int n = *lvl_ctr(L, L.level - 1);
+    return L.seg > 1 && L.level >= 1 && (L.seg_max <= 0 || n <= L.seg_max) &&
+           (long long)n * L.seg <= (long long)L.rows * (long long)L.cam.width;
 }
 
 // Walk pass, segmented: K = L.seg lanes per ray, lane = (ray lane / K, segment lane % K);
