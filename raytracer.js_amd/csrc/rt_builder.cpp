@@ -57,6 +57,8 @@ struct rt_builder {
     size_t synced_nodes = 0, synced_ents = 0;
     std::vector<int> j_nodes, j_child, j_ents;
     bool j_full = false;               // an edit the journal cannot express (replaced child, outward growth)
+    std::vector<int32_t> sub;          // nodes in each node's subtree (DFS ids without a traversal)
+    size_t unreached = 0;              // nodes the last full sync did not reach (replaced subtrees)
 };
 
 using namespace rtjs;
@@ -69,6 +71,8 @@ static int new_node(rt_builder *b, const double pos[3], double size, int parent)
     n.parent = parent;
     for (int i = 0; i < 8; i++) n.child[i] = -1;
     b->nodes.push_back(std::move(n));
+    b->sub.push_back(1);
+    for (int a = parent; a >= 0; a = b->nodes[a].parent) b->sub[a]++;
     return (int)b->nodes.size() - 1;
 }
 
@@ -202,6 +206,7 @@ static int extend_outside(rt_builder *b, int root, int node, const double a[3], 
         int np = new_node(b, pp, psize, -1);
         b->nodes[np].child[idx] = cur;
         b->nodes[cur].parent = np;
+        b->sub[np] += b->sub[cur];
         cur = np;
         if (aabb_in_cube(a, asize, pp, psize)) return cur;
         cur_depth++;
@@ -443,10 +448,9 @@ int rt_builder_edit(rt_builder *b, const RtSceneStore *st, uint64_t epoch, const
     const int N = (int)b->nodes.size();
     const int n_old = (int)b->synced_nodes;
     // new nodes take the next slots in creation order; every node is reachable (no child was replaced)
+    if (b->unreached) return 1;                  // a node the last full sync did not reach
     b->slot.resize(N);
     for (int n = n_old; n < N; n++) b->slot[n] = n;
-    for (int n = 0; n < N; n++)
-        if (b->slot[n] < 0) return 1;            // a node the last full sync did not reach
     e = RtEdit{};
     e.n_slots = N;
     e.n_entities = (int32_t)b->ents.size();
@@ -493,18 +497,27 @@ int rt_builder_edit(rt_builder *b, const RtSceneStore *st, uint64_t epoch, const
         e.sub_ent.push_back(id);
         e.sub_val.push_back(b->ents[id].substance);
     }
-    // DFS numbering (the node ids the outputs report) changes only when nodes were created
+    // DFS numbering (the node ids the outputs report) changes only when nodes were created: each new
+    // node's id from the subtree sizes along its path (O(depth)), and for the existing nodes the
+    // shift G (an old id a becomes a + #{j : G_j <= a}, G_j = F_j - j over the new ids F, ascending),
+    // applied on the device
     if (N > n_old) {
-        e.dfs.assign(N, -1);
-        std::vector<int> stack{b->root};
-        int k = 0;
-        while (!stack.empty()) {
-            const int t = stack.back();
-            stack.pop_back();
-            e.dfs[b->slot[t]] = k++;
-            for (int c = 7; c >= 0; c--)
-                if (b->nodes[t].child[c] >= 0) stack.push_back(b->nodes[t].child[c]);
+        std::vector<int32_t> F;
+        for (int n = n_old; n < N; n++) {
+            int32_t id = 0;
+            for (int x = n; x != b->root;) {
+                const int p = b->nodes[x].parent;
+                id += 1;
+                for (int c = 0; c < 8 && b->nodes[p].child[c] != x; c++)
+                    if (b->nodes[p].child[c] >= 0) id += b->sub[b->nodes[p].child[c]];
+                x = p;
+            }
+            e.dfs_new_slot.push_back(b->slot[n]);
+            e.dfs_new_val.push_back(id);
+            F.push_back(id);
         }
+        std::sort(F.begin(), F.end());
+        for (size_t j = 0; j < F.size(); j++) e.dfs_shift.push_back(F[j] - (int32_t)j);
     }
     // a rough mirror is listed: only scenes whose shade table has one pay the entity scan
     bool any = false;
@@ -520,6 +533,14 @@ void rt_builder_synced(rt_builder *b, const RtSceneStore *st, uint64_t epoch, bo
     if (full) {                                  // a full upload numbers the slots in DFS order
         b->slot.assign(b->nodes.size(), -1);
         for (size_t k = 0; k < b->l_order.size(); k++) b->slot[b->l_order[k]] = (int32_t)k;
+        b->unreached = b->nodes.size() - b->l_order.size();
+        // subtree sizes of the reachable tree (a replaced child leaves its old subtree counted)
+        b->sub.assign(b->nodes.size(), 0);
+        for (size_t k = b->l_order.size(); k-- > 0;) {
+            const int n = b->l_order[k];
+            b->sub[n] += 1;
+            if (n != b->root && b->nodes[n].parent >= 0) b->sub[b->nodes[n].parent] += b->sub[n];
+        }
     }
     b->synced_nodes = b->nodes.size();
     b->synced_ents = b->ents.size();

@@ -133,7 +133,9 @@ struct RtEdit {
     std::vector<int32_t> set_ent, set_type, set_shade;    // per member
     std::vector<double> set_geom;                         // 9 per member (rt_scene_desc.ent_geom layout)
     std::vector<int32_t> sub_ent, sub_val;                // entities whose substance is (re)sent
-    std::vector<int32_t> dfs;              // node_dfs of every slot when the DFS numbering changed, else empty
+    // DFS ids (node_dfs) when nodes were created: the new slots' ids, and the shift of the existing
+    // ones (old id a -> a + #{j : dfs_shift[j] <= a}; ascending), applied by a device kernel
+    std::vector<int32_t> dfs_new_slot, dfs_new_val, dfs_shift;
     bool scatter = false;                  // a rough mirror is listed
 };
 // 0: `out` holds the edit since the builder's sync with (st, epoch); 1: a full upload is needed

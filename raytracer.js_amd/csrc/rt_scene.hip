@@ -88,6 +88,21 @@ __global__ void __launch_bounds__(256) k_scene_patch(const Chunk *__restrict__ c
     for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
 }
 
+// node_dfs of the existing slots after an edit created nodes: old id a -> a + #{j : G_j <= a}.
+__global__ void __launch_bounds__(256) k_dfs_shift(int32_t *__restrict__ dfs, int n, const int32_t *__restrict__ G, int k)
+{
+    for (int s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
+        const int a = dfs[s];
+        int lo = 0, hi = k;                      // upper bound of a in G
+        while (lo < hi) {
+            const int m = (lo + hi) >> 1;
+            if (G[m] <= a) lo = m + 1;
+            else hi = m;
+        }
+        dfs[s] = a + lo;
+    }
+}
+
 using Key = std::array<uint64_t, 4>;
 struct KeyHash {
     size_t operator()(const Key &k) const
@@ -276,6 +291,9 @@ struct RtSceneStore {
     std::vector<uint8_t> stage;
     struct Pending { int arr; size_t off, bytes, src; };
     std::vector<Pending> pend;
+    // a node_dfs shift for the next flush: G at stage offset shift_at, k entries, over shift_n slots
+    size_t shift_at = 0;
+    int shift_k = 0, shift_n = 0;
 
     ~RtSceneStore()
     {
@@ -338,7 +356,7 @@ struct RtSceneStore {
     int flush(int64_t *bytes_out)
     {
         const size_t nch = pend.size();
-        if (!nch) return RT_OK;
+        if (!nch && !shift_k) return RT_OK;
         // pinned: [staged bytes | chunk table of device 0 | ... of device ndev-1]; each device gets
         // the staged bytes and its own table (the destination addresses differ), so all devices'
         // copies and scatter kernels run concurrently
@@ -366,6 +384,12 @@ struct RtSceneStore {
             uint8_t *dev = (uint8_t *)dstage[d].p;
             HIP_TRY(hipMemcpyAsync(dev, pinned, tab, hipMemcpyHostToDevice, sd));
             HIP_TRY(hipMemcpyAsync(dev + tab, pinned + tab + (size_t)d * tsz, tsz, hipMemcpyHostToDevice, sd));
+            if (shift_k > 0 && shift_n > 0) {        // the existing slots' DFS ids (new slots are patched)
+                const unsigned nb = (unsigned)std::min(1024, (shift_n + 255) / 256);
+                hipLaunchKernelGGL(k_dfs_shift, dim3(nb), dim3(256), 0, sd, (int32_t *)a[d][A_NODE_DFS].p, shift_n,
+                                   reinterpret_cast<const int32_t *>(dev + shift_at), shift_k);
+                HIP_TRY(hipGetLastError());
+            }
             for (size_t k0 = 0; k0 < nch; k0 += 65535) {
                 const unsigned nb = (unsigned)std::min<size_t>(65535, nch - k0);
                 hipLaunchKernelGGL(k_scene_patch, dim3(nb), dim3(256), 0, sd,
@@ -378,6 +402,7 @@ struct RtSceneStore {
         if (r != RT_OK) return r;
         stage.clear();
         pend.clear();
+        shift_k = shift_n = 0;
         return RT_OK;
     }
 
@@ -871,7 +896,26 @@ struct RtSceneStore {
             add(A_ENT_SUB, 4 * (size_t)e.sub_ent[i], &e.sub_val[i], 4 * (j - i));
             i = j;
         }
-        if (!e.dfs.empty()) diff_runs(A_NODE_DFS, e.dfs, m_dfs, 1);
+        if (!e.dfs_new_slot.empty()) {
+            // new slots: their ids, as runs; existing slots: the shift kernel in flush (m_dfs is not kept:
+            // desc_mirrors goes false below, and a full upload rebuilds it)
+            std::vector<int32_t> order(e.dfs_new_slot.size());
+            for (size_t i = 0; i < order.size(); i++) order[i] = (int32_t)i;
+            std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return e.dfs_new_slot[x] < e.dfs_new_slot[y]; });
+            std::vector<int32_t> sl, val;
+            for (int32_t i : order) { sl.push_back(e.dfs_new_slot[i]); val.push_back(e.dfs_new_val[i]); }
+            for (size_t i = 0; i < sl.size();) {
+                size_t j = i + 1;
+                while (j < sl.size() && sl[j] == sl[j - 1] + 1) j++;
+                add(A_NODE_DFS, 4 * (size_t)sl[i], &val[i], 4 * (j - i));
+                i = j;
+            }
+            shift_at = (stage.size() + 15) & ~(size_t)15;
+            stage.resize(shift_at + 4 * e.dfs_shift.size());
+            memcpy(stage.data() + shift_at, e.dfs_shift.data(), 4 * e.dfs_shift.size());
+            shift_k = (int)e.dfs_shift.size();
+            shift_n = (int)n_old;
+        }
         if (m_shades.size() != (size_t)ns || (ns && memcmp(m_shades.data(), shades, sizeof(rt_shade) * ns) != 0)) {
             m_shades.assign(shades, shades + ns);
             add(A_SHADES, 0, m_shades.data(), sizeof(rt_shade) * m_shades.size());
