@@ -106,6 +106,7 @@ struct rt_ctx {
     int refill = 16;                 // wide bounce levels walked with per-lane refill (RT_REFILL; 0: off)
     bool refill_always = false;      // RT_REFILL_ALWAYS=1: also levels no recent frame showed wide (tests)
     int seg_max = 64 * 4096;         // bounce levels of more rays run unsegmented, refilled (RT_SEG_MAX; 0: no limit)
+    bool hints = true;               // size bounce-level grids from a recent frame (RT_HINTS=0: full grids)
     int occ = 0;
     int diag = 0;
     bool has_scene = false;
@@ -183,6 +184,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_REFILL")) c->refill = atoi(e) < 0 ? 0 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_REFILL_ALWAYS")) c->refill_always = atoi(e) != 0;
     if (const char *e = getenv("RT_SEG_MAX")) c->seg_max = atoi(e) < 0 ? 0 : atoi(e);
+    if (const char *e = getenv("RT_HINTS")) c->hints = atoi(e) != 0;
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
@@ -405,7 +407,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     if (!d.h_ctr && hipHostMalloc((void **)&d.h_ctr, sizeof(int32_t) * RT_CTR_INTS, hipHostMallocDefault) == hipSuccess)
         for (int i = 0; i < RT_CTR_INTS; i++) d.h_ctr[i] = -1;        // unknown until a frame completes
     (void)hipGetLastError();
-    L.ctr_hint = d.h_ctr;
+    L.ctr_hint = c->hints ? d.h_ctr : nullptr;
     L.occ = c->occ;
     L.diag = c->diag;
     L.cont_group = c->cont_group;
