@@ -28,6 +28,9 @@ namespace {
 
 constexpr int ST_OK = 0, ST_WARN = 1, ST_FAULT = 2, ST_CAP = 3;
 constexpr int ST_DEFER = 100;                    // split path: continuation queued, pixel written later
+#ifndef RT_EARLY_SHADE
+#define RT_EARLY_SHADE 1
+#endif
 constexpr int STEP_CAP = 1 << 24;                // per-walk loop bound: every lane terminates
 
 // ---- node access --------------------------------------------------------------------------------
@@ -1220,6 +1223,24 @@ __device__ __forceinline__ void ray_src(const RtLaunch &L, int item, int lane, R
     }
 }
 
+// Level 0's shading queue (k_first -> k_shade, RT_EARLY_SHADE): its length, in a free slot of the
+// level's counter block; the entries (pixel ids of this part) live in ray_cn, unused at level 0.
+__device__ __forceinline__ int32_t *shade_n(const RtLaunch &L) { return lvl_ctr(L, 0) + 1; }
+
+// The primary ray of pixel `id` of this part (row-major within the part), as ray_src gives it.
+__device__ __forceinline__ void pixel_src(const RtLaunch &L, int id, RaySrc &r)
+{
+    const int W = L.cam.width;
+    const int lr = id / W, x = id - lr * W;
+    r.valid = true;
+    r.rec = nullptr;
+    r.id = (size_t)id;
+    r.pix = id;
+    const size_t plane = (size_t)L.rows * (size_t)W;
+    const size_t di = (size_t)x * (size_t)L.rows + (size_t)lr;           // x-major (k_frame_start)
+    for (int i = 0; i < 3; i++) { r.o[i] = L.cam.pos[i]; r.d[i] = L.dirs[(size_t)i * plane + di]; }
+}
+
 // One lane per pixel of this part; 256-lane blocks cover 16x16 pixel tiles, each wave an 8x8 tile.
 // Persistent waves: each wave repeatedly takes the next 8x8 pixel tile from an atomic queue
 // (one returning atomic per tile, lane 0) and traces it one ray per lane.  Per-ray cost varies by
@@ -1557,6 +1578,48 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
 // the candidate scan lives here: its cull traversal is a chain of dependent loads, and a lane
 // pays the sum of its own node tests rather than, as in the fused kernel, the maximum over the
 // wave at every walker stop.
+// Level 0 of the first-hit pass ends the rays whose bounce is terminal and plain, so the shading
+// pass only sees the others: a primary ray that hits nothing (sky), or whose first hit is a light or
+// a matte (REFLECTION, not a mirror) surface without an image texture and not at an acute normal.
+// The colour is trace_ray's for that case, in its operation order (col starts at 1: 1 * x == x; path
+// starts at +0).  Returns false for every other ray, which k_shade shades as before; a ray ended
+// here gets first = {-2, -2}.
+__device__ __forceinline__ bool early_shade(const RtLaunch &L, const RaySrc &src, int cn, int2 hit, RayResult &R)
+{
+    const RtDevScene &S = L.scene;
+    const rt_config_desc &cfg = L.cfg;
+    R.segments = 1;
+    R.status = ST_OK;
+    if (hit.y < 0) {
+        if ((cn & 3) != 0 || cfg.sky_image) return false;      // the walk threw / capped, or a textured sky
+        R.hit_ent = -1;
+        R.hit_node = -1;
+        R.rgb[0] = 1.0 * cfg.sky_rgb[0]; R.rgb[1] = 1.0 * cfg.sky_rgb[1]; R.rgb[2] = 1.0 * cfg.sky_rgb[2];
+        return true;
+    }
+    const RtPrim &pr = S.prim[hit.y];
+    Hit h;
+    if (prim_hit(pr, src.o, src.d, h) != 1) return false;
+    if (dot3(src.d[0], src.d[1], src.d[2], h.n[0], h.n[1], h.n[2]) >= 0) return false;     // the warn case
+    const rt_shade sh = S.shades[pr.meta >> 2];
+    if (sh.image) return false;
+    double c0 = 1.0 * sh.rgb[0], c1 = 1.0 * sh.rgb[1], c2 = 1.0 * sh.rgb[2];
+    if (sh.light) {
+        const double a = h.p[0] - src.o[0], b = h.p[1] - src.o[1], e = h.p[2] - src.o[2];
+        double path = 0;
+        path += sqrt(dot3(a, b, e, a, b, e));
+        const double t = path * cfg.distance_attenuation_factor;
+        const double isl = 1.0 / (2.220446049250313e-16 + t * t);
+        c0 = c0 * isl; c1 = c1 * isl; c2 = c2 * isl;
+    } else if (!(sh.response == RT_RESP_REFLECTION && !sh.mirror)) {
+        return false;                                          // mirror, transmission: k_shade
+    }
+    R.hit_ent = S.list_entity[pr.rank];
+    R.hit_node = hit.x;
+    R.rgb[0] = c0; R.rgb[1] = c1; R.rgb[2] = c2;
+    return true;
+}
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
 {
@@ -1592,6 +1655,13 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
                 if (hk >= 0) { res = make_int2(node, hk); break; }
             }
         }
+        if (RT_EARLY_SHADE && L.level == 0) {
+            // level 0: end the plain terminal rays here; queue the rest for k_shade (ray_cn is free at
+            // level 0), wave by wave so a shading wave keeps a tile's rays together
+            RayResult R;
+            if (!(cn >= 0 && !fault && early_shade(L, src, cn, res, R))) L.ray_cn[wave_reserve(shade_n(L))] = (int)src.id;
+            else write_pixel(L, (size_t)src.pix, R);
+        }
         reinterpret_cast<int2 *>(L.first)[src.id] = res;
         }
     }
@@ -1609,13 +1679,22 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
     const RayQueues Q = {L.queue[L.level & 1], lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
     const int ch = L.claim_chunk;
     const int32_t *ray_cn = seg_mode(L) ? L.ray_cn : L.cand_n;     // segmented levels: k_first's combined status
+    const bool queued = RT_EARLY_SHADE && L.level == 0;             // level 0: the rays k_first queued
+    const int n_q = queued ? *shade_n(L) : 0;
+    const int n_it = queued ? (n_q + 63) >> 6 : items;
     for (;;) {
         int t_end;
-        const int t0 = claim_xcd(pass_heads(L, L.level, 3), items, lane, ch, t_end, L.xcd_mask & 4);
-        if (t0 >= items) break;
+        const int t0 = claim_xcd(pass_heads(L, L.level, 3), n_it, lane, ch, t_end, L.xcd_mask & 4);
+        if (t0 >= n_it) break;
         for (int t = t0; t < t_end; t++) {
         RaySrc src;
-        ray_src(L, t, lane, src);
+        if (queued) {
+            const int q = t * 64 + lane;
+            src.valid = q < n_q;
+            if (src.valid) pixel_src(L, L.ray_cn[q], src);
+        } else {
+            ray_src(L, t, lane, src);
+        }
         if (!src.valid) continue;
         RayResult R;
         if (F.fault) {
