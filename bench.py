@@ -356,9 +356,7 @@ def exposure_bench(ctx, frame, stream, reps=20):
                 mean=st.mean, variance=st.variance, range=[lo, hi])
 
 
-def host_frame_time(ctx, cam, cfg, segments, warm=3, reps=10):
-    """SURVEY §8(d) ms/frame: rt_trace_frame with a host Float32Array (camera in, kernels, gather,
-    D2H into the ebuffer) — what the JS drop-in's trace_frame() costs.  Median of `reps` after `warm`."""
+def _host_frame_ms(ctx, cam, cfg, warm, reps):
     rgb = np.zeros(cam.width * cam.height * 3, np.float32)
     for _ in range(warm):
         ctx.trace_frame(cam, cfg, rgb=rgb, ids=False, stats=False)
@@ -367,10 +365,40 @@ def host_frame_time(ctx, cam, cfg, segments, warm=3, reps=10):
         t0 = time.perf_counter()
         ctx.trace_frame(cam, cfg, rgb=rgb, ids=False, stats=False)
         ts.append((time.perf_counter() - t0) * 1e3)
+    return ts, rgb
+
+
+def host_frame_time(ctx, cam, cfg, segments, scene=None, device=0, warm=3, reps=10):
+    """SURVEY §8(d) ms/frame: rt_trace_frame with a host Float32Array (camera in, kernels, D2H into
+    the ebuffer) — what the JS drop-in's trace_frame() costs.  Median of `reps` after `warm`.  The
+    context runs the frame as row bands on their own streams (RT_BANDS, default 2; DESIGN.md §5.14);
+    with `scene`, a second context with RT_BANDS=1 (one launch sequence, then one D2H) is timed
+    beside it and must produce the identical frame."""
+    ts, rgb = _host_frame_ms(ctx, cam, cfg, warm, reps)
     med = float(np.median(ts))
-    return dict(entry="rt_trace_frame (host RGB buffer, D2H included)", warmup=warm, frames=reps,
-                ms_per_frame_median=round(med, 3), ms_min=round(min(ts), 3), ms_max=round(max(ts), 3),
-                value=round(segments / (med * 1e-3) / 1e6, 3), unit="Mrays/s")
+    out = dict(entry="rt_trace_frame (host RGB buffer, D2H included)", warmup=warm, frames=reps,
+               bands=int(os.environ.get("RT_BANDS", "2")),
+               ms_per_frame_median=round(med, 3), ms_min=round(min(ts), 3), ms_max=round(max(ts), 3),
+               value=round(segments / (med * 1e-3) / 1e6, 3), unit="Mrays/s")
+    if scene is not None:
+        prev = os.environ.get("RT_BANDS")
+        os.environ["RT_BANDS"] = "1"
+        try:
+            one = rtamd.Context(device)
+        finally:
+            if prev is None:
+                del os.environ["RT_BANDS"]
+            else:
+                os.environ["RT_BANDS"] = prev
+        try:
+            one.upload(scene)
+            ts1, rgb1 = _host_frame_ms(one, cam, cfg, warm, reps)
+        finally:
+            one.close()
+        med1 = float(np.median(ts1))
+        out["one_launch"] = dict(ms_per_frame_median=round(med1, 3), value=round(segments / (med1 * 1e-3) / 1e6, 3),
+                                 identical=bool(np.array_equal(rgb.view(np.uint32), rgb1.view(np.uint32))))
+    return out
 
 
 def pmc_child(args):
@@ -467,7 +495,7 @@ def run_ranks(args, spec, scene, W, H, refmax, world, rank, local):
     kt = ctx.kernel_times(args.steps)
     extra = dict(mode="one process per GPU" if world > 1 else "one GPU", collective="torch.distributed.gather (%s)" % (
                  "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()) if world > 1 else None, n_gpus=dist.get_world_size() if world > 1 else 1)
-    host = host_frame_time(ctx, cam, cfg, tot["segments"]) if rank == 0 and world == 1 else None
+    host = host_frame_time(ctx, cam, cfg, tot["segments"], scene, local) if rank == 0 and world == 1 else None
     expo = exposure_bench(ctx, sg.frame, stream) if rank == 0 else None
     out = dict(res, tot=tot, counters=counters, same=same, kernel_ms=float(np.mean(kt)) if len(kt) else None,
                host=host, exposure=expo, P=P, **extra)

@@ -120,7 +120,33 @@ struct rt_ctx {
     // on dev[0]: the stacked parts (gather target) and, for host-buffer frames, the assembled frame
     DevBuf g_stack, g_frame, g_hit_e, g_hit_n, g_status;
     DevBuf b_stat, b_walk;           // exposure statistics, debug walks (dev[0])
+    // host-buffer frames on one GPU run as row bands on their own streams (trace_frame_bands)
+    int bands = 2;                   // RT_BANDS (1: one launch sequence per frame)
+    int band_order = 0;              // RT_BAND_ORDER: bit 0 level-0 walks in band order, bit 1 stream
+                                     // priorities by band (both measured slower or neutral, §5.14)
+    int n_band = 0;                  // band states initialised
+    RtDevice band[RT_MAX_BANDS];     // streams and pass buffers of the bands (dev[0]'s GPU and scene)
+    int32_t *h_fault = nullptr;      // pinned: each band's fault flag
+    hipEvent_t band_walk[RT_MAX_BANDS] = {};   // each band's level-0 walk done (RT_BAND_ORDER bit 0)
 };
+
+static void release_device(RtDevice &d)
+{
+    (void)hipSetDevice(d.device);
+    for (DevBuf *b : {&d.b_cand, &d.b_cand_n, &d.b_first, &d.b_queue, &d.b_ctr, &d.b_setup, &d.b_dirs, &d.b_rgb,
+                      &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault})
+        b->release();
+    for (auto &e : d.ev)
+        for (hipEvent_t x : e)
+            if (x) (void)hipEventDestroy(x);
+    d.ev.clear();
+    if (d.sync) (void)hipEventDestroy(d.sync);
+    if (d.h_ctr) (void)hipHostFree(d.h_ctr);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+    d.sync = nullptr;
+    d.h_ctr = nullptr;
+    d.stream = nullptr;
+}
 
 static int use_device(const RtDevice &d)
 {
@@ -187,6 +213,8 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_HINTS")) c->hints = atoi(e) != 0;
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
+    if (const char *e = getenv("RT_BAND_ORDER")) c->band_order = atoi(e) & 3;
+    if (const char *e = getenv("RT_BANDS")) c->bands = atoi(e) < 1 ? 1 : (atoi(e) > RT_MAX_BANDS ? RT_MAX_BANDS : atoi(e));
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
     // parts on one GPU) gathers by device copies, as RT_CREATE_PEER_GATHER asks for.  RT_GATHER
     // (rccl / peer) forces a mode, also for one device (tests on a one-GPU host).
@@ -251,6 +279,8 @@ extern "C" void rt_destroy(rt_ctx *c)
         (void)hipSetDevice(c->dev[k].device);
         if (c->dev[k].stream) (void)hipStreamSynchronize(c->dev[k].stream);
     }
+    for (int b = 0; b < RT_MAX_BANDS; b++)
+        if (c->band[b].stream) (void)hipStreamSynchronize(c->band[b].stream);
     if (c->gather == RT_GATHER_RCCL) {
         const RtRccl *R = rt_rccl();
         for (int k = 0; R && k < c->n_dev; k++)
@@ -261,19 +291,11 @@ extern "C" void rt_destroy(rt_ctx *c)
     (void)hipSetDevice(c->dev[0].device);
     for (DevBuf *b : {&c->g_stack, &c->g_frame, &c->g_hit_e, &c->g_hit_n, &c->g_status, &c->b_stat, &c->b_walk})
         b->release();
-    for (int k = 0; k < c->n_dev; k++) {
-        RtDevice &d = c->dev[k];
-        (void)hipSetDevice(d.device);
-        for (DevBuf *b : {&d.b_cand, &d.b_cand_n, &d.b_first, &d.b_queue, &d.b_ctr, &d.b_setup, &d.b_dirs, &d.b_rgb,
-                          &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault})
-            b->release();
-        for (auto &e : d.ev)
-            for (hipEvent_t x : e)
-                if (x) (void)hipEventDestroy(x);
-        if (d.sync) (void)hipEventDestroy(d.sync);
-        if (d.h_ctr) (void)hipHostFree(d.h_ctr);
-        if (d.stream) (void)hipStreamDestroy(d.stream);
-    }
+    for (int b = 0; b < RT_MAX_BANDS; b++) release_device(c->band[b]);
+    if (c->h_fault) (void)hipHostFree(c->h_fault);
+    for (hipEvent_t e : c->band_walk)
+        if (e) (void)hipEventDestroy(e);
+    for (int k = 0; k < c->n_dev; k++) release_device(c->dev[k]);
     delete c;
 }
 
@@ -375,11 +397,13 @@ static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_confi
 // d.b_rgb / d.b_hit_* unless the caller repoints L.rgb.  Device d must be current.
 enum { WANT_IDS = 1, WANT_STATUS = 2 };
 
+// A part's launch: its rows are the part's stripes (rt_part_rows), or, for a band (band_rows >= 0),
+// frame rows row0 .. row0 + band_rows - 1.
 static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_config_desc *cfg, int part,
-                   int n_parts, int stripe, int want, RtLaunch &L)
+                   int n_parts, int stripe, int want, RtLaunch &L, int row0 = 0, int band_rows = -1)
 {
     const bool want_ids = want & WANT_IDS, want_status = want & (WANT_IDS | WANT_STATUS);
-    const int rows = rt_part_rows(cam->height, part, n_parts, stripe);
+    const int rows = band_rows >= 0 ? band_rows : rt_part_rows(cam->height, part, n_parts, stripe);
     const size_t P = (size_t)rows * (size_t)cam->width;
     int r;
     if ((r = d.b_dirs.ensure(sizeof(double) * 3 * (P ? P : 1))) != RT_OK) return r;
@@ -396,6 +420,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.n_parts = n_parts;
     L.stripe_rows = stripe;
     L.rows = rows;
+    L.row0 = row0;
     L.setup = (RtFrameSetup *)d.b_setup.p;
     L.dirs = (double *)d.b_dirs.p;
     L.hit_entity = want_ids ? (int32_t *)d.b_hit_e.p : nullptr;
@@ -658,6 +683,147 @@ static inline int64_t scan_index(int x, int y, int W, int H)
     return ry * W + rx;
 }
 
+
+// The reference's frame ends at its first throwing pixel (status 2; a step-capped ray, 3, counts as
+// one): pixels before it in scan order take the frame's new colour (`fresh`), it and later ones keep
+// the old one (`rgb_inout`).
+static void keep_after_first_throw(float *rgb_inout, const float *fresh, const uint8_t *st_host, int W, int H)
+{
+    int64_t first = (int64_t)W * H;
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            if (st_host[(size_t)y * W + x] >= 2) first = std::min(first, scan_index(x, y, W, H));
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            if (scan_index(x, y, W, H) < first) {
+                const size_t i = 3 * ((size_t)y * W + x);
+                rgb_inout[i] = fresh[i];
+                rgb_inout[i + 1] = fresh[i + 1];
+                rgb_inout[i + 2] = fresh[i + 2];
+            }
+}
+
+// Row bands of a host-buffer frame on one GPU, in the reference's scan order (rows from the centre
+// row down, then from the centre up): bands [hh, H) top to bottom, then [0, hh) bottom to top, with
+// boundaries on multiples of 8 rows from the centre (whole 8x8 tiles).  Returns the band count.
+static int band_layout(int H, int nb, int row0[], int rows[])
+{
+    const int hh = H >> 1, lo = (nb + 1) / 2, hi = nb - lo;
+    int n = 0;
+    auto cut = [](int span, int k, int parts) { return std::min(span, ((int)((long long)span * k / parts) + 7) & ~7); };
+    for (int k = 0; k < lo; k++) {                       // [hh, H)
+        const int a = cut(H - hh, k, lo), b = cut(H - hh, k + 1, lo);
+        if (b > a) { row0[n] = hh + a; rows[n] = b - a; n++; }
+    }
+    for (int k = 0; k < hi; k++) {                       // [0, hh), from the centre up
+        const int a = cut(hh, k, hi), b = cut(hh, k + 1, hi);
+        if (b > a) { row0[n] = hh - b; rows[n] = b - a; n++; }
+    }
+    return n;
+}
+
+static int init_bands(rt_ctx *c, int nb)
+{
+    for (int b = c->n_band; b < nb; b++) {
+        RtDevice &d = c->band[b];
+        d.device = c->dev[0].device;
+        // earlier bands (in scan order, copied out first) take the higher stream priorities
+        int least = 0, greatest = 0;
+        if (!(c->band_order & 2) || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+        const int prio = nb > 1 ? greatest + (int)((long long)(least - greatest) * b / (nb - 1)) : greatest;
+        HIP_TRY(hipStreamCreateWithPriority(&d.stream, hipStreamNonBlocking, prio));
+        d.ev.assign(2, {nullptr, nullptr});
+        for (auto &e : d.ev) {
+            HIP_TRY(hipEventCreate(&e[0]));
+            HIP_TRY(hipEventCreate(&e[1]));
+        }
+        HIP_TRY(hipEventCreateWithFlags(&d.sync, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->band_walk[b], hipEventDisableTiming));
+        int r;
+        if ((r = d.b_setup.ensure(sizeof(RtFrameSetup))) != RT_OK) return r;
+        if ((r = d.b_fault.ensure(sizeof(int))) != RT_OK) return r;
+        if ((r = d.b_ctr.ensure(sizeof(int32_t) * RT_CTR_INTS)) != RT_OK) return r;
+        c->n_band = b + 1;
+    }
+    if (!c->h_fault) HIP_TRY(hipHostMalloc((void **)&c->h_fault, sizeof(int32_t) * RT_MAX_BANDS, hipHostMallocDefault));
+    return RT_OK;
+}
+
+// rt_trace_frame on one GPU without counters: the frame's rows as bands (band_layout), each band's
+// passes on its own stream, so that a band's latency tail overlaps the next band's work and a finished
+// band's D2H into the host buffer overlaps the bands still tracing.  Bands are copied out in scan
+// order; from the first band that faulted on, the frame is finished as the one-launch path does it
+// (earlier bands hold no throwing pixel, so they are final when copied).
+static int trace_frame_bands(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,
+                             int32_t *hit_entity, int32_t *hit_node, uint8_t *status, int nb_want)
+{
+    RtDevice &d0 = c->dev[0];
+    const int W = cam->width, H = cam->height;
+    const size_t P = (size_t)W * (size_t)H;
+    const bool ids = hit_entity || hit_node;
+    const bool blend = cfg->col_weight != 1.0;
+    int row0[RT_MAX_BANDS], rows[RT_MAX_BANDS];
+    const int nb = band_layout(H, nb_want, row0, rows);
+    int r;
+    if ((r = init_bands(c, nb)) != RT_OK) return r;
+    if ((r = d0.b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
+    if ((r = d0.b_status.ensure(P)) != RT_OK) return r;
+    if (ids && ((r = d0.b_hit_e.ensure(sizeof(int32_t) * P)) != RT_OK || (r = d0.b_hit_n.ensure(sizeof(int32_t) * P)) != RT_OK))
+        return r;
+    float *f_rgb = (float *)d0.b_rgb.p;
+    uint8_t *f_st = (uint8_t *)d0.b_status.p;
+    int32_t *f_he = ids ? (int32_t *)d0.b_hit_e.p : nullptr, *f_hn = ids ? (int32_t *)d0.b_hit_n.p : nullptr;
+    // queue every band before copying any out
+    for (int b = 0; b < nb; b++) {
+        RtDevice &d = c->band[b];
+        d.scene = d0.scene;
+        RtLaunch L;
+        if ((r = prepare(c, d, cam, cfg, 0, 1, H, 0, L, row0[b], rows[b])) != RT_OK) return r;
+        const size_t off = (size_t)row0[b] * W, n = (size_t)rows[b] * W;
+        L.rgb = f_rgb + 3 * off;
+        L.status = f_st + off;
+        L.hit_entity = f_he ? f_he + off : nullptr;
+        L.hit_node = f_hn ? f_hn + off : nullptr;
+        if (blend) HIP_TRY(hipMemcpyAsync(L.rgb, rgb_inout + 3 * off, sizeof(float) * 3 * n, hipMemcpyHostToDevice, d.stream));
+        HIP_TRY(hipMemsetAsync(d.b_fault.p, 0, sizeof(int), d.stream));
+        hipEvent_t *ev = next_events(d);
+        const bool order = (c->band_order & 1) != 0;
+        if ((r = rt_launch_frame(L, d.stream, ev[0], ev[1], order && b > 0 ? c->band_walk[b - 1] : nullptr,
+                                 order ? c->band_walk[b] : nullptr)) != RT_OK)
+            return r;
+        HIP_TRY(hipMemcpyAsync(&c->h_fault[b], d.b_fault.p, sizeof(int32_t), hipMemcpyDeviceToHost, d.stream));
+        HIP_TRY(hipEventRecord(d.sync, d.stream));
+    }
+    int fb = nb;                                         // first band (scan order) with a throwing pixel
+    for (int b = 0; b < nb; b++) {
+        RtDevice &d = c->band[b];
+        HIP_TRY(hipEventSynchronize(d.sync));
+        if (c->h_fault[b]) { fb = b; break; }
+        const size_t off = (size_t)row0[b] * W, n = (size_t)rows[b] * W;
+        HIP_TRY(hipMemcpyAsync(rgb_inout + 3 * off, f_rgb + 3 * off, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, d.stream));
+        if (hit_entity) HIP_TRY(hipMemcpyAsync(hit_entity + off, f_he + off, sizeof(int32_t) * n, hipMemcpyDeviceToHost, d.stream));
+        if (hit_node) HIP_TRY(hipMemcpyAsync(hit_node + off, f_hn + off, sizeof(int32_t) * n, hipMemcpyDeviceToHost, d.stream));
+        if (status) HIP_TRY(hipMemcpyAsync(status + off, f_st + off, n, hipMemcpyDeviceToHost, d.stream));
+    }
+    for (int b = 0; b < nb; b++) HIP_TRY(hipStreamSynchronize(c->band[b].stream));
+    if (fb == nb) return RT_OK;
+    // a faulting frame: the whole frame's colours and status, then the reference's partial frame
+    std::vector<uint8_t> st_tmp;
+    uint8_t *st_host = status;
+    if (!st_host) {
+        st_tmp.resize(P);
+        st_host = st_tmp.data();
+    }
+    std::vector<float> fresh(3 * P);
+    HIP_TRY(hipMemcpy(fresh.data(), f_rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(st_host, f_st, P, hipMemcpyDeviceToHost));
+    if (hit_entity) HIP_TRY(hipMemcpy(hit_entity, f_he, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
+    if (hit_node) HIP_TRY(hipMemcpy(hit_node, f_hn, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
+    keep_after_first_throw(rgb_inout, fresh.data(), st_host, W, H);
+    return rt_set_error(RT_E_FAULT, "a ray reached a state where the reference throws (status 2/3 pixels); "
+                                    "pixels from the first one in scan order on keep their previous value");
+}
+
 extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,
                               int32_t *hit_entity, int32_t *hit_node, uint8_t *status, rt_stats *stats)
 {
@@ -673,6 +839,8 @@ extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     const size_t P = (size_t)W * (size_t)H;
     const bool blend = cfg->col_weight != 1.0;
     FrameOut o = {};
+    if (c->gather == RT_GATHER_NONE && !stats && c->bands > 1 && c->split && H >= 16)
+        return trace_frame_bands(c, cam, cfg, rgb_inout, hit_entity, hit_node, status, c->bands);
     if (c->gather == RT_GATHER_NONE) {
         RtLaunch L;
         // per-pixel status always: it locates the first throwing pixel of a faulting frame
@@ -717,22 +885,7 @@ extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     if (hit_node) HIP_TRY(hipMemcpyAsync(hit_node, o.hit_n, sizeof(int32_t) * P, hipMemcpyDeviceToHost, d0.stream));
     if (st_host) HIP_TRY(hipMemcpyAsync(st_host, o.status, P, hipMemcpyDeviceToHost, d0.stream));
     HIP_TRY(hipStreamSynchronize(d0.stream));
-    if (fault) {
-        // the reference's frame ends at its first throwing pixel (status 2; a step-capped ray, 3,
-        // counts as one): earlier pixels take the new colour, it and later ones keep the old
-        int64_t first = (int64_t)P;
-        for (int y = 0; y < H; y++)
-            for (int x = 0; x < W; x++)
-                if (st_host[(size_t)y * W + x] >= 2) first = std::min(first, scan_index(x, y, W, H));
-        for (int y = 0; y < H; y++)
-            for (int x = 0; x < W; x++)
-                if (scan_index(x, y, W, H) < first) {
-                    const size_t i = 3 * ((size_t)y * W + x);
-                    rgb_inout[i] = fresh[i];
-                    rgb_inout[i + 1] = fresh[i + 1];
-                    rgb_inout[i + 2] = fresh[i + 2];
-                }
-    }
+    if (fault) keep_after_first_throw(rgb_inout, fresh.data(), st_host, W, H);
     if (stats) stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (fault) return rt_set_error(RT_E_FAULT, "a ray reached a state where the reference throws (status 2/3 pixels); "
                                                "pixels from the first one in scan order on keep their previous value");

@@ -154,6 +154,7 @@ struct RtLaunch {
     rt_camera_desc cam;
     rt_config_desc cfg;
     int32_t part, n_parts, stripe_rows, rows;   // this part's row set
+    int32_t row0;                               // first frame row of a band (host-frame bands; else 0)
     RtFrameSetup *setup;                        // device
     double *dirs;                               // device [3][rows*W] (SoA planes)
     float *rgb;                                 // device [rows*W*3]
@@ -191,7 +192,10 @@ struct RtLaunch {
 
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };
 
-int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end);
+// walk_wait / walk_done (host-frame bands): the level-0 walk pass waits for event walk_wait (the
+// previous band's level-0 walk) and walk_done is recorded after it, so bands' walks run in order.
+int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end, void *walk_wait = nullptr,
+                    void *walk_done = nullptr);
 // rt_exposure.hip: statistics into d_out3 = {mean, variance, absdev} (d_partials: 2 * n_blocks doubles)
 int rt_launch_exposure_stats(const float *d_rgb, long long n, double *d_partials, int n_blocks, double *d_out3,
                              void *stream);
@@ -223,6 +227,8 @@ const RtRccl *rt_rccl(void);        // null when librccl is unavailable (rt_rccl
 const char *rt_rccl_error(void);
 
 // Row bookkeeping for the stripe partition.
+#define RT_MAX_BANDS 8   // row bands of a host-buffer frame on one GPU (rt_api.hip trace_frame_bands)
+
 static inline int32_t rt_part_rows(int32_t H, int32_t part, int32_t n_parts, int32_t stripe)
 {
     int32_t n_stripes = (H + stripe - 1) / stripe, rows = 0;

@@ -747,7 +747,7 @@ __device__ __forceinline__ void rotate_1(double &x, double &y, double c, double 
 
 __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
                                                      RtFrameSetup *setup, int part, int n_parts, int stripe,
-                                                     int rows, double *__restrict__ dirs)
+                                                     int rows, int row0, double *__restrict__ dirs)
 {
     const int lane = threadIdx.x & 63;
     if (blockIdx.x == 0) {
@@ -784,7 +784,7 @@ __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_des
     const int i = hc >> 1;                    // component
     const bool right = (hc & 1) == 0;
     const int W = cam.width, H = cam.height;
-    const int y = part_row_to_y(lr, part, n_parts, stripe);
+    const int y = row0 + part_row_to_y(lr, part, n_parts, stripe);
     // iter_v(H>>1, H, rot_scan_v_v, 1, false) / iter_v((H>>1)-1, -1, counter, -1, true): the row's
     // direction is fr after y - H/2 rotations (top), or after the counter pre-rotation and
     // H/2 - 1 - y more (bottom)
@@ -883,7 +883,8 @@ __device__ __forceinline__ uint64_t frame_pixel(const RtLaunch &L, int pix)
 {
     const int W = L.cam.width;
     const int lr = pix / W;
-    return (uint64_t)part_row_to_y(lr, L.part, L.n_parts, L.stripe_rows) * (uint64_t)W + (uint64_t)(pix - lr * W);
+    return (uint64_t)(L.row0 + part_row_to_y(lr, L.part, L.n_parts, L.stripe_rows)) * (uint64_t)W +
+           (uint64_t)(pix - lr * W);
 }
 
 // Ray.scatter_ray (src/raytracer.ts:121-133) with counter draws (include/rt.h RT_SCATTER_COUNTER):
@@ -1827,14 +1828,14 @@ static int level_blocks(const RtLaunch &L, int32_t hint_rays)
     return (int)std::min<long long>(std::max<long long>(256, est), 1 << 20);
 }
 
-int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end)
+int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_end, void *walk_wait, void *walk_done)
 {
     hipStream_t st = (hipStream_t)stream;
     const int W = L.cam.width;
     const int rg_lanes = 6 * (L.rows > 0 ? L.rows : 0);
     (void)hipGetLastError();                     // a stale error of an earlier runtime call is not ours
     hipLaunchKernelGGL(k_frame_start, dim3(1 + (rg_lanes + 255) / 256), dim3(256), 0, st, L.scene, L.cam, L.cfg,
-                       L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.dirs);
+                       L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.row0, L.dirs);
     HIP_TRY(hipGetLastError());
     if (L.rows <= 0 || L.skip_trace) {           // an empty part (more devices than stripes): no trace
         if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
@@ -1866,8 +1867,10 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             const int mb = lv >= 1 ? level_blocks(L, hint) : 0;
             // per-lane refill only where a recent frame had a wide level (both walk kernels read Lv.refill)
             Lv.refill = L.refill_always || hint > 64 * 4096 ? L.refill : 0;
+            if (lv == 0 && walk_wait) HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)walk_wait, 0));
             launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
+            if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
             if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lv, mb);     // one of the two runs (§5.10)
             if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<4>, st, Lv, mb);
             launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv, mb);

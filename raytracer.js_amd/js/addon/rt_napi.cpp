@@ -5,6 +5,7 @@
 // synchronous and blocks the event loop exactly like the reference's Raytracer.trace_frame()
 // (src/raytracer.ts:308-330).  A negative RT_E_* code becomes a thrown JS Error whose `code` is
 // the RT_E_* name, matching the reference's "errors are thrown JS Errors" contract.
+#include <chrono>
 #include <node_api.h>
 #include <stdio.h>
 #include <string.h>
@@ -328,10 +329,13 @@ napi_value set_num(napi_env env, napi_value obj, const char *k, double v)
 
 napi_value TraceFrame(napi_env env, napi_callback_info info)
 {
-    size_t argc = 7;
-    napi_value argv[7];
+    size_t argc = 8;
+    napi_value argv[8];
     NAPI_TRY(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
-    if (argc < 4) { napi_throw_error(env, "RT_E_INVALID", "traceFrame(ctx, cam, cfg, pixels[, hitEntity, hitNode, status])"); return nullptr; }
+    if (argc < 4) {
+        napi_throw_error(env, "RT_E_INVALID", "traceFrame(ctx, cam, cfg, pixels[, hitEntity, hitNode, status, wantStats])");
+        return nullptr;
+    }
     rt_ctx *ctx = unwrap(env, argv[0]);
     if (!ctx) return nullptr;
     rt_camera_desc cam;
@@ -384,13 +388,27 @@ napi_value TraceFrame(napi_env env, napi_callback_info info)
         napi_throw_error(env, "RT_E_INVALID", "id buffers must have width*height elements");
         return nullptr;
     }
+    // work counters are opt-in (wantStats): counting runs the fused stats kernel, not the split
+    // passes, so a plain frame only reports its wall time
+    bool want_stats = false;
+    if (argc > 7) {
+        napi_valuetype vt;
+        napi_typeof(env, argv[7], &vt);
+        if (vt == napi_boolean) napi_get_value_bool(env, argv[7], &want_stats);
+    }
     rt_stats stats;
     memset(&stats, 0, sizeof stats);
+    const auto t0 = std::chrono::steady_clock::now();
     const int rc = rt_trace_frame(ctx, &cam, &cfg, (float *)px.data, has_he ? (int32_t *)he.data : nullptr,
-                                  has_hn ? (int32_t *)hn.data : nullptr, has_st ? (uint8_t *)st.data : nullptr, &stats);
+                                  has_hn ? (int32_t *)hn.data : nullptr, has_st ? (uint8_t *)st.data : nullptr,
+                                  want_stats ? &stats : nullptr);
     if (throw_rc(env, rc)) return nullptr;
     napi_value out;
     napi_create_object(env, &out);
+    if (!want_stats) {
+        set_num(env, out, "frame_ms", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        return out;
+    }
     set_num(env, out, "segments", (double)stats.segments);
     set_num(env, out, "n_ret", (double)stats.n_ret);
     set_num(env, out, "n_slot", (double)stats.n_slot);

@@ -23,17 +23,26 @@ export interface RaytracerConfig {
   distance_attenuation_factor: number;
 }
 
+/** Work counters of a frame (options.stats); without them only frame_ms is set. */
 export interface RtStats {
-  segments: number; n_ret: number; n_slot: number; n_loc: number; n_sph: number; n_box: number;
-  n_tri: number; n_hit: number; primary: number; n_warn: number; n_fault: number;
-  kernel_ms: number; frame_ms: number;
+  segments?: number; n_ret?: number; n_slot?: number; n_loc?: number; n_sph?: number; n_box?: number;
+  n_tri?: number; n_hit?: number; primary?: number; n_warn?: number; n_fault?: number;
+  kernel_ms?: number; frame_ms: number;
 }
 
 export interface RaytracerOptions {
   /** HIP device ordinal (default 0) */
   device?: number;
+  /** GPUs to split every frame over (row stripes, RCCL gather to devices[0]) */
+  devices?: number[];
+  /** rows per stripe of the multi-device split (default 8) */
+  stripe_rows?: number;
   /** keep per-pixel primary hit entity / node ids and status after each frame */
   keep_ids?: boolean;
+  /** fill last_stats with work counters (runs the slower fused counting kernel) */
+  stats?: boolean;
+  /** 'counter': rough mirrors with the counter-based RNG (include/rt.h RT_SCATTER_COUNTER) */
+  scatter?: 'counter';
 }
 
 /** Drop-in for the reference `Raytracer`: same constructor and methods; trace_frame() runs on a GPU. */

@@ -258,7 +258,10 @@ class Raytracer {
 	 * scene, the parts gathered on devices[0] over RCCL and copied into the ebuffer once.
 	 * `options.scatter === 'counter'` renders rough mirrors with the counter-based RNG (include/rt.h
 	 * RT_SCATTER_COUNTER), keyed each frame by one draw of this Raytracer's rng; otherwise they are
-	 * rejected (RT_E_UNSUPPORTED), as scatter_ray's sequential PRNG cannot be reproduced in parallel. */
+	 * rejected (RT_E_UNSUPPORTED), as scatter_ray's sequential PRNG cannot be reproduced in parallel.
+	 * `options.stats` fills `last_stats` with the frame's work counters (segments, walker steps,
+	 * entity tests); counting runs the slower fused kernel, so without it `last_stats` holds only
+	 * `frame_ms`. */
 	constructor(config, otree, camera, ebuffer, rng, options) {
 		this.camera = camera;
 		this.ebuffer = ebuffer;
@@ -338,9 +341,9 @@ class Raytracer {
 				this.last_status = new Uint8Array(P);
 			}
 			this.last_stats = a.traceFrame(this._ctx, cam, cfg, eb.pixels, this.last_hit_entity,
-				this.last_hit_node, this.last_status);
+				this.last_hit_node, this.last_status, !!this.options.stats);
 		} else {
-			this.last_stats = a.traceFrame(this._ctx, cam, cfg, eb.pixels);
+			this.last_stats = a.traceFrame(this._ctx, cam, cfg, eb.pixels, null, null, null, !!this.options.stats);
 		}
 		if (typeof eb.clean_cache === 'function') eb.clean_cache();  // set_color_i invalidates the stats cache
 	}

@@ -1,6 +1,6 @@
 /*
  * run_dropin.js <scene.json> <out_prefix> [--serialize-only] [--scatter <seed>] [--edit A B C]
- *               [--devices 0,0,0]
+ *               [--devices 0,0,0] [--repeat N]
  * Builds reference-shaped objects, checks serialize_scene() reproduces the linearised arrays, and
  * (unless --serialize-only) renders one frame with the drop-in Raytracer into ExposureBuffer.pixels.
  * --scatter: rough mirrors with options.scatter = 'counter', the rng's one draw = seed / 2^53.
@@ -10,6 +10,8 @@
  *   EntitySet, which is where add_entity_to_octree files a cube straddling the centre planes), and
  *   entity B takes entity C's material and texture (set_material / set_texture).
  * --devices: options.devices (one context over several GPUs, or several parts on one GPU).
+ * --repeat N: after the first frame, N frames timed each with options.stats off, then N with it on
+ *   (<out_prefix>.repeat.json).
  */
 'use strict';
 const fs = require('fs');
@@ -56,7 +58,7 @@ const si = process.argv.indexOf('--scatter');
 const seed = si > 0 ? Number(process.argv[si + 1]) : null;
 const rng = seed === null ? null : { next: () => seed / 9007199254740992 };
 const di = process.argv.indexOf('--devices');
-const opts = seed === null ? { keep_ids: true } : { keep_ids: true, scatter: 'counter' };
+const opts = seed === null ? { keep_ids: true, stats: true } : { keep_ids: true, stats: true, scatter: 'counter' };
 if (di > 0) opts.devices = process.argv[di + 1].split(',').map(Number);
 const tracer = new rt.Raytracer(config, world.root, cam, eb, rng, opts);
 const t0 = process.hrtime.bigint();
@@ -77,6 +79,25 @@ function write_frame(prefix, extra) {
 	fs.writeFileSync(prefix + '.node', Buffer.from(tracer.last_hit_node.buffer));
 	fs.writeFileSync(prefix + '.status', Buffer.from(tracer.last_status.buffer));
 	fs.writeFileSync(prefix + '.json', JSON.stringify(Object.assign({ stats: tracer.last_stats }, extra)));
+}
+
+// --repeat N: N more frames timed one by one, without and then with the work counters
+const ri = process.argv.indexOf('--repeat');
+if (ri > 0) {
+	const n = Number(process.argv[ri + 1]);
+	const times = (stats) => {
+		tracer.options.stats = stats;
+		tracer.options.keep_ids = false;                        // the reference's trace_frame: pixels only
+		const ms = [];
+		for (let i = 0; i < n; i++) {
+			const a = process.hrtime.bigint();
+			tracer.trace_frame();
+			ms.push(Number(process.hrtime.bigint() - a) / 1e6);
+		}
+		return ms;
+	};
+	const plain = times(false), counted = times(true);
+	fs.writeFileSync(out_prefix + '.repeat.json', JSON.stringify({ frame_ms: plain, frame_ms_stats: counted }));
 }
 
 const ei = process.argv.indexOf('--edit');
