@@ -401,6 +401,26 @@ def host_frame_time(ctx, cam, cfg, segments, scene=None, device=0, warm=3, reps=
     return out
 
 
+def js_frame(args, timeout_s=300):
+    """The JS drop-in's trace_frame() (node -> N-API -> librt, ExposureBuffer.pixels filled), median of
+    10 frames, run by tools/js_frame_time.py in a child node process; also timed with options.stats
+    (the work counters' fused kernel).  None without node or the addon."""
+    tool = os.path.join(ROOT, "tools", "js_frame_time.py")
+    if shutil.which("node") is None or not os.path.exists(tool):
+        return None
+    try:
+        r = subprocess.run([sys.executable, tool, "--config", args.config, "--frames", "10"], capture_output=True,
+                           text=True, timeout=timeout_s)
+        if r.returncode != 0:
+            return dict(error=(r.stdout + r.stderr)[-400:])
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        return dict(entry="Raytracer.trace_frame() on node (raytracer.js_amd/js)", frames=d["frames"],
+                    ms_per_frame_median=d["js_trace_frame_ms_median"],
+                    ms_per_frame_median_with_stats=d["js_trace_frame_ms_median_with_stats"])
+    except (subprocess.TimeoutExpired, ValueError, KeyError, IndexError) as e:
+        return dict(error=str(e)[-400:])
+
+
 def pmc_child(args):
     """Minimal frame loop profiled by the rocprofv3 passes: no stats launch, no CPU baseline, no output."""
     factory, W, H, refmax = scenes.WORKLOADS[args.config]
@@ -588,6 +608,7 @@ def main():
                     help="skip the rocprofv3 kernel-trace / PMC passes")
     ap.add_argument("--profile-out", default=None, help="keep the rocprofv3 summaries (kernel stats, PMC) here")
     ap.add_argument("--inflight", type=int, default=0, help="frames in flight (contexts / streams); 0 = default")
+    ap.add_argument("--no-js", action="store_true", help="skip the JS drop-in trace_frame() timing")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
@@ -659,6 +680,7 @@ def main():
             roofline["profile_notes"] = [x for x in [err] + notes if x]
 
     cpu = cpu_baseline(spec, scene, cam, cfg, args.cpu_budget) if args.cpu_budget > 0 and n_gpus == 1 else None
+    js = js_frame(args) if n_gpus == 1 and not args.no_js else None
     rec = {
         "metric": "Mrays/s (whole node) at %dx%d" % (W, H),
         "value": round(value, 3),
@@ -681,6 +703,7 @@ def main():
         "roofline": roofline,
         "serial": serial,
         "host_frame": res["host"],
+        "js_frame": js,
         "cpu_baseline": cpu,
         "exposure": res["exposure"],
         "mpixels_per_s": round(W * H * steps / el / 1e6, 3),

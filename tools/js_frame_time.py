@@ -13,12 +13,34 @@ import tempfile
 from pathlib import Path
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "raytracer.js_amd", "python"), ROOT, os.path.join(ROOT, "tests")]
+sys.path[:0] = [os.path.join(ROOT, "raytracer.js_amd", "python")]
 
 import numpy as np  # noqa: E402
 
+import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
-from test_js_dropin import RUNNER, _dump  # noqa: E402
+
+RUNNER = os.path.join(ROOT, "tests", "js", "run_dropin.js")
+
+
+def _dump(tmp_path, spec, cam, cfg):
+    """The scene, camera and config as the JSON run_dropin.js inflates into reference-shaped objects
+    (the same format as tests/test_js_dropin.py writes)."""
+    s = rtamd.build_scene(spec)
+    sc = {k: getattr(s, k).tolist() for k in ("node_pos", "node_size", "node_parent", "node_child", "node_ent_begin",
+                                             "node_ent_count", "list_entity", "ent_type", "ent_geom", "ent_shade",
+                                             "ent_substance", "substance_ri")}
+    sc["shades"] = [dict(response=int(x["response"]), light=int(x["light"]), mirror=int(x["mirror"]),
+                         roughness=float(x["roughness"]), image=int(x["image"]), rgb=[float(v) for v in x["rgb"]])
+                    for x in s.shades]
+    sc["images"] = [dict(width=int(im.shape[1]), height=int(im.shape[0]), rgb=im.reshape(-1).tolist()) for im in s.images]
+    sc["cam"] = dict(width=cam.width, height=cam.height, pos=list(cam.pos), fr=list(cam.fr), lf=list(cam.lf),
+                     up=list(cam.up), scan_h=list(cam.scan_h), scan_v=list(cam.scan_v))
+    sc["cfg"] = dict(refmax=cfg.refmax, default_substance=cfg.default_substance, atten=cfg.distance_attenuation_factor,
+                     sky=list(cfg.sky_rgb), sky_image=int(cfg.sky_image))
+    p = tmp_path / "scene.json"
+    p.write_text(json.dumps(sc))
+    return str(p)
 
 
 def main():
