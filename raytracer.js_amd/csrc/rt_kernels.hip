@@ -466,12 +466,16 @@ __device__ __forceinline__ void walker_trip(const RtDevScene &S, Walker &w, Emit
     }
 }
 
+#ifndef RT_TRIP_UNROLL
+#define RT_TRIP_UNROLL 1
+#endif
 template <bool STOP, bool ALL_FAST, typename Emit>
 __device__ __forceinline__ int walker_run_t(const RtDevScene &S, Walker &w, Emit &&emit, int stop)
 {
     int res = w.cur_tree >= 0 ? 1 : 0;
     do {
-        walker_trip<STOP, ALL_FAST>(S, w, emit, stop, res);
+#pragma unroll
+        for (int u = 0; u < RT_TRIP_UNROLL; u++) walker_trip<STOP, ALL_FAST>(S, w, emit, stop, res);
     } while (__ballot(res == 1));
     return res;
 }
