@@ -306,11 +306,12 @@ def test_split_equals_fused(ctx, name, monkeypatch):
             c.close()
 
 
-@pytest.mark.parametrize("group", ["1", "16", "64"])
+@pytest.mark.parametrize("group", ["1", "3", "16", "48", "64"])
 def test_continuation_rays_per_wave(ctx, group, monkeypatch):
     """Bounce levels take RT_CONT_GROUP rays per wave, up to 64 when a level is large (cont_g:
     config 5's millions of bounce rays); the width changes scheduling, not results.  Unsegmented
-    levels (RT_SEG=0), refmax 5, mirrors and transmission: identical to the oracle."""
+    levels (RT_SEG=0), refmax 5, mirrors and transmission: identical to the oracle.  3 and 48 are
+    not powers of two (rt_create rounds them down to 2 and 32; cont_g never exceeds 64)."""
     spec = _transmission_spec()
     cam, cfg = scenes.make_camera(160, 120), scenes.make_config(5)
     monkeypatch.setenv("RT_SEG", "0")
