@@ -377,7 +377,8 @@ def host_frame_time(ctx, cam, cfg, segments, scene=None, device=0, warm=3, reps=
     ts, rgb = _host_frame_ms(ctx, cam, cfg, warm, reps)
     med = float(np.median(ts))
     out = dict(entry="rt_trace_frame (host RGB buffer, D2H included)", warmup=warm, frames=reps,
-               bands=int(os.environ.get("RT_BANDS", "2")),
+               bands=int(os.environ.get("RT_BANDS", "2")) if cam.width * cam.height >= int(
+                   os.environ.get("RT_BAND_MIN", str(1 << 20))) else 1,
                ms_per_frame_median=round(med, 3), ms_min=round(min(ts), 3), ms_max=round(max(ts), 3),
                value=round(segments / (med * 1e-3) / 1e6, 3), unit="Mrays/s")
     if scene is not None:

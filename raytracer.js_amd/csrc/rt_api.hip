@@ -124,6 +124,8 @@ struct rt_ctx {
     int bands = 2;                   // RT_BANDS (1: one launch sequence per frame)
     int band_order = 0;              // RT_BAND_ORDER: bit 0 level-0 walks in band order, bit 1 stream
                                      // priorities by band (both measured slower or neutral, §5.14)
+    int64_t band_min = 1 << 20;      // RT_BAND_MIN: frames of fewer pixels run as one launch (256^2: 0.44 ms
+                                     // one launch against 0.61 in 2 bands; 1080p and up gain, §5.14)
     int n_band = 0;                  // band states initialised
     RtDevice band[RT_MAX_BANDS];     // streams and pass buffers of the bands (dev[0]'s GPU and scene)
     int32_t *h_fault = nullptr;      // pinned: each band's fault flag
@@ -213,6 +215,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_HINTS")) c->hints = atoi(e) != 0;
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
+    if (const char *e = getenv("RT_BAND_MIN")) c->band_min = atoll(e) < 0 ? 0 : atoll(e);
     if (const char *e = getenv("RT_BAND_ORDER")) c->band_order = atoi(e) & 3;
     if (const char *e = getenv("RT_BANDS")) c->bands = atoi(e) < 1 ? 1 : (atoi(e) > RT_MAX_BANDS ? RT_MAX_BANDS : atoi(e));
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
@@ -839,7 +842,7 @@ extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     const size_t P = (size_t)W * (size_t)H;
     const bool blend = cfg->col_weight != 1.0;
     FrameOut o = {};
-    if (c->gather == RT_GATHER_NONE && !stats && c->bands > 1 && c->split && H >= 16)
+    if (c->gather == RT_GATHER_NONE && !stats && c->bands > 1 && c->split && H >= 16 && (int64_t)P >= c->band_min)
         return trace_frame_bands(c, cam, cfg, rgb_inout, hit_entity, hit_node, status, c->bands);
     if (c->gather == RT_GATHER_NONE) {
         RtLaunch L;

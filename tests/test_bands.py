@@ -27,6 +27,7 @@ def _same(a, b):
 def _ctx(scene, bands, monkeypatch, order=0):
     monkeypatch.setenv("RT_BANDS", str(bands))
     monkeypatch.setenv("RT_BAND_ORDER", str(order))
+    monkeypatch.setenv("RT_BAND_MIN", "0")          # bands at test sizes (the default starts at 2^20 pixels)
     c = rtamd.Context(0)
     c.upload(scene)
     return c
