@@ -37,6 +37,9 @@ Prints ONE JSON line on rank 0.  Beside `value` it reports:
                 this process may use, with the host CPU model; the C oracle's timing beside it.
 """
 import os
+import time
+
+_T_START = time.monotonic()        # the whole run's deadline counts from here (imports included)
 
 # hardware queues for the frames in flight, read once when the HIP runtime initialises: at least
 # 16 (HIP's default, and the GPU box's setting, is 4; DESIGN.md §7)
@@ -52,9 +55,10 @@ import math
 import re
 import shutil
 import subprocess
+import signal
 import sys
 import tempfile
-import time
+import threading
 
 import numpy as np
 import torch
@@ -99,6 +103,116 @@ PMC_PASSES = {
 
 def algorithmic_bytes(counters, table):
     return sum(table[k] * counters[k] for k in table)
+
+
+# ---- wall-time bound -----------------------------------------------------------------------------------
+# The driver kills a bench that runs past its window (600 s).  Every phase after the timed frames is
+# optional and bounded: each child process runs in its own session under its own time limit and is
+# killed with its whole process group when that runs out; the phases share one deadline
+# (--deadline, 420 s from the interpreter's start by default), and a watchdog thread prints the record
+# gathered so far and exits once the deadline plus a grace period has passed, whatever is still running.
+class Deadline:
+    def __init__(self, total_s, t0=None):
+        self.t0 = _T_START if t0 is None else t0
+        self.end = self.t0 + total_s
+
+    def left(self):
+        return self.end - time.monotonic()
+
+    def slice(self, cap_s, reserve_s=0.0):
+        """Seconds a phase may take: at most cap_s, and never into the last reserve_s."""
+        return max(0.0, min(cap_s, self.left() - reserve_s))
+
+
+_CHILD_LOCK = threading.Lock()
+_CHILDREN = set()
+
+
+def _kill_group(p):
+    try:
+        os.killpg(p.pid, signal.SIGKILL)
+    except (ProcessLookupError, PermissionError):
+        pass
+    try:
+        p.wait(timeout=10)
+    except subprocess.TimeoutExpired:
+        pass
+
+
+def run_bounded(cmd, timeout_s, env=None):
+    """Run cmd in a new session, stdout+stderr into a temporary file (no pipe a grandchild could hold
+    open).  At timeout_s the whole process group is killed.  Returns (exit code or None on timeout,
+    output text)."""
+    with tempfile.TemporaryFile() as out:
+        p = subprocess.Popen(cmd, stdout=out, stderr=subprocess.STDOUT, env=env, start_new_session=True)
+        with _CHILD_LOCK:
+            _CHILDREN.add(p)
+        try:
+            rc = p.wait(timeout=max(timeout_s, 0.5))
+        except subprocess.TimeoutExpired:
+            _kill_group(p)
+            rc = None
+        finally:
+            with _CHILD_LOCK:
+                _CHILDREN.discard(p)
+        out.seek(0)
+        return rc, out.read().decode(errors="replace")
+
+
+class Reporter:
+    """Prints the one JSON line exactly once: from the main thread when every phase is done, or from the
+    watchdog at the hard deadline with whatever the record holds then (phases not reached are named in
+    `skipped_phases`)."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.rec = None
+        self.printed = False
+        self.phase = "gpu"
+
+    def set(self, rec):
+        with self.lock:
+            self.rec = rec
+
+    def update(self, key, value):
+        with self.lock:
+            self.rec[key] = value
+
+    def update_wall(self, key):
+        with self.lock:
+            self.rec["wall"] = dict(self.rec["wall"], **{key: round(time.monotonic() - _T_START, 1)})
+
+    def emit(self, note=None):
+        with self.lock:
+            if self.printed or self.rec is None:
+                return False
+            if note:
+                self.rec["skipped_phases"] = self.rec.get("skipped_phases", []) + [note]
+                self.rec["wall"] = dict(self.rec["wall"], emitted_s=round(time.monotonic() - _T_START, 1))
+            print(json.dumps(self.rec), flush=True)
+            self.printed = True
+            return True
+
+    def arm(self, deadline, grace_s=30.0):
+        def fire():
+            wait = deadline.left() + grace_s
+            while wait > 0:
+                time.sleep(min(wait, 1.0))
+                wait = deadline.left() + grace_s
+                if self.printed:
+                    return
+            with _CHILD_LOCK:
+                kids = list(_CHILDREN)
+            for p in kids:
+                _kill_group(p)
+            ok = self.emit("watchdog: deadline passed during phase %r" % self.phase)
+            if not ok and not self.printed:
+                print("bench.py: deadline passed before the timed frames finished (phase %r)" % self.phase,
+                      file=sys.stderr, flush=True)
+            os._exit(0 if (ok or self.printed) else 3)
+        t = threading.Thread(target=fire, name="bench-watchdog", daemon=True)
+        t.start()
+        return t
 
 
 # ---- CPU baseline ------------------------------------------------------------------------------------
@@ -156,7 +270,7 @@ def cpu_baseline_c(spec, cam, cfg, budget_s):
                               sample="the same pixels on %d threads (all usable cores), %.2f s" % (nt, t_mt)))
 
 
-def cpu_baseline_js(scene, cam, cfg, budget_s):
+def cpu_baseline_js(scene, cam, cfg, budget_s, deadline, reserve_s):
     """The path restated in JavaScript on the reference's object model (oracle/js/rt_path.js), run by
     node: 1 thread on a random pixel sample sized for ~budget_s, then a worker_threads split of a
     larger sample over every usable core (BASELINE.md CPU-baseline plan).  Bit-identical to the C
@@ -168,17 +282,20 @@ def cpu_baseline_js(scene, cam, cfg, budget_s):
     P = cam.width * cam.height
     order = np.random.default_rng(1).permutation(P).astype(np.int32)
     tmp = tempfile.mkdtemp(prefix="rt_jsb_")
+    # each node run: the scene build in JS plus the sample; limits scale with the budget and stop at
+    # the deadline (a run that hits its limit raises TimeoutExpired: the caller falls back to C)
+    lim = lambda: deadline.slice(max(30.0, 4 * budget_s), reserve_s)
     try:
-        js_baseline.export(scene, cam, cfg, order[:4096], tmp)            # calibration (JIT warm-up included)
-        info, _ = js_baseline.run(tmp, threads=1)
+        js_baseline.export(scene, cam, cfg, order[:1024], tmp)            # calibration (JIT warm-up included)
+        info, _ = js_baseline.run(tmp, threads=1, timeout=lim())
         rate = max(info["segments"] / info["trace_s"], 1.0)
-        n1 = int(min(P, max(4096, rate * budget_s)))
+        n1 = int(min(P, max(1024, rate * budget_s)))
         js_baseline.export(scene, cam, cfg, order[:n1], tmp)
-        i1, _ = js_baseline.run(tmp, threads=1, timeout=max(120, 6 * budget_s))
+        i1, _ = js_baseline.run(tmp, threads=1, timeout=lim())
         nt, visible, quota = usable_cores()
         nm = int(min(P, max(n1, rate * budget_s * nt / 2)))
         js_baseline.export(scene, cam, cfg, order[:nm], tmp)
-        im, _ = js_baseline.run(tmp, threads=nt, timeout=max(120, 6 * budget_s))
+        im, _ = js_baseline.run(tmp, threads=nt, timeout=lim())
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     return dict(value=i1["segments"] / i1["trace_s"] / 1e6, unit="Mrays/s", cores=1, kind="port",
@@ -191,16 +308,25 @@ def cpu_baseline_js(scene, cam, cfg, budget_s):
                 node_os_cpus=i1["cpus"])
 
 
-def cpu_baseline(spec, scene, cam, cfg, budget_s):
+def cpu_baseline(spec, scene, cam, cfg, budget_s, deadline, reserve_s=0.0):
     """cpu_baseline: the JavaScript restatement on node (the reference's own language and object
-    model) when node is present, with the C oracle's timing beside it under `c_oracle`."""
+    model) when node is present, with the C oracle's timing beside it under `c_oracle`.  The budget
+    shrinks to what the deadline leaves; a JS run that hits its limit is reported under `js_error`
+    and the C oracle's timing becomes the baseline."""
     nt, visible, quota = usable_cores()
-    js = cpu_baseline_js(scene, cam, cfg, budget_s / 2)
+    budget_s = max(1.0, min(budget_s, deadline.slice(budget_s * 4, reserve_s) / 4))
+    js, js_err = None, None
+    try:
+        js = cpu_baseline_js(scene, cam, cfg, budget_s / 2, deadline, reserve_s)
+    except (subprocess.TimeoutExpired, RuntimeError, ValueError, OSError) as e:
+        js_err = "%s: %s" % (type(e).__name__, str(e)[-300:])
     c = cpu_baseline_c(spec, cam, cfg, budget_s / 2 if js else budget_s)
     out = js if js else c
     out.update(cpu_model=cpu_model(), cpus_visible=visible, cpu_quota=quota)
     if js:
         out["c_oracle"] = c
+    if js_err:
+        out["js_error"] = js_err
     return out
 
 
@@ -223,22 +349,29 @@ def _rocprof(extra, args, timeout_s, keep=None):
     out = tempfile.mkdtemp(prefix="rt_prof_")
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     cmd = [prof] + extra + ["-d", out, "-o", "p", "--output-format", "csv", "--"] + _child_cmd(args)
-    try:
-        r = subprocess.run(cmd, env=env, timeout=timeout_s, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
-    except subprocess.TimeoutExpired:
+    if timeout_s < 5:
         shutil.rmtree(out, ignore_errors=True)
-        return None, "%s: timed out" % " ".join(extra[:2])
-    if r.returncode != 0:
-        tail = r.stdout.decode(errors="replace").strip().splitlines()[-3:]
+        return None, "%s: skipped, %.0f s left of the bench deadline" % (" ".join(extra[:2]), timeout_s)
+    t0 = time.monotonic()
+    rc, text = run_bounded(cmd, timeout_s, env=env)
+    if rc is None:
         shutil.rmtree(out, ignore_errors=True)
-        return None, "%s: exit %d: %s" % (" ".join(extra[:2]), r.returncode, " | ".join(tail))
+        return None, "%s: killed at its %.0f s limit" % (" ".join(extra[:2]), timeout_s)
+    if rc != 0:
+        tail = text.strip().splitlines()[-3:]
+        shutil.rmtree(out, ignore_errors=True)
+        return None, "%s: exit %d: %s" % (" ".join(extra[:2]), rc, " | ".join(tail))
+    _PROF_WALL.append(round(time.monotonic() - t0, 1))
     return out, None
 
 
-def kernel_durations(args, timeout_s=300):
+_PROF_WALL = []          # wall seconds of each completed rocprofv3 pass (reported in the record)
+
+
+def kernel_durations(args, deadline, cap_s=60.0, reserve_s=0.0):
     """Per-kernel time per frame (ms) from rocprofv3 --kernel-trace --stats over PMC_FRAMES frames;
     the stats CSV is kept under --profile-out."""
-    out, err = _rocprof(["--kernel-trace", "--stats"], args, timeout_s)
+    out, err = _rocprof(["--kernel-trace", "--stats"], args, deadline.slice(cap_s, reserve_s))
     if err:
         return None, err
     try:
@@ -260,12 +393,13 @@ def kernel_durations(args, timeout_s=300):
         shutil.rmtree(out, ignore_errors=True)
 
 
-def pmc_counters(args, timeout_s=300):
+def pmc_counters(args, deadline, cap_s=60.0, reserve_s=0.0):
     """Counter totals per frame and trace kernel over the PMC_PASSES (one rocprofv3 --pmc run each:
-    counter slots per block are limited; MI355X_MICROARCH.md)."""
+    counter slots per block are limited; MI355X_MICROARCH.md).  Each pass gets at most cap_s; passes
+    that no longer fit the deadline are skipped and named in the notes."""
     tot, notes = {}, []
     for name, counters in PMC_PASSES.items():
-        out, err = _rocprof(["--pmc"] + counters, args, timeout_s)
+        out, err = _rocprof(["--pmc"] + counters, args, deadline.slice(cap_s, reserve_s))
         if err:
             notes.append(err)
             continue
@@ -319,8 +453,7 @@ def kernel_rooflines(dur, pmc, counters):
             # the pass's algorithmic bytes are shared by its kernels in proportion to their time
             share = ms / sum(v for kk, v in dur.items() if KERNEL_PASS.get(kk) == p)
             ab = algorithmic_bytes(counters, PASS_BYTES[p]) * share
-            e.update(alg_bytes_cache_served=int(ab), alg_GBps=round(ab / s / 1e9, 1),
-                     alg_frac_of_hbm_peak=round(ab / s / 1e9 / HBM_PEAK_GBS, 4))
+            e.update(alg_bytes_cache_served=int(ab), alg_GBps=round(ab / s / 1e9, 1))
         roofs = {r: e[f] for r, f in (("valu-issue", "valu_issue_frac"), ("hbm", "hbm_frac")) if f in e}
         if roofs:
             e["binding_roof"] = max(roofs, key=roofs.get)
@@ -402,23 +535,26 @@ def host_frame_time(ctx, cam, cfg, segments, scene=None, device=0, warm=3, reps=
     return out
 
 
-def js_frame(args, timeout_s=300):
+def js_frame(args, timeout_s):
     """The JS drop-in's trace_frame() (node -> N-API -> librt, ExposureBuffer.pixels filled), median of
     10 frames, run by tools/js_frame_time.py in a child node process; also timed with options.stats
     (the work counters' fused kernel).  None without node or the addon."""
     tool = os.path.join(ROOT, "tools", "js_frame_time.py")
     if shutil.which("node") is None or not os.path.exists(tool):
         return None
+    if timeout_s < 10:
+        return dict(error="skipped: %.0f s left of the bench deadline" % timeout_s)
     try:
-        r = subprocess.run([sys.executable, tool, "--config", args.config, "--frames", "10"], capture_output=True,
-                           text=True, timeout=timeout_s)
-        if r.returncode != 0:
-            return dict(error=(r.stdout + r.stderr)[-400:])
-        d = json.loads(r.stdout.strip().splitlines()[-1])
+        rc, text = run_bounded([sys.executable, tool, "--config", args.config, "--frames", "10"], timeout_s)
+        if rc is None:
+            return dict(error="killed at its %.0f s limit" % timeout_s)
+        if rc != 0:
+            return dict(error=text[-400:])
+        d = json.loads([ln for ln in text.strip().splitlines() if ln.startswith("{")][-1])
         return dict(entry="Raytracer.trace_frame() on node (raytracer.js_amd/js)", frames=d["frames"],
                     ms_per_frame_median=d["js_trace_frame_ms_median"],
                     ms_per_frame_median_with_stats=d["js_trace_frame_ms_median_with_stats"])
-    except (subprocess.TimeoutExpired, ValueError, KeyError, IndexError) as e:
+    except (ValueError, KeyError, IndexError) as e:
         return dict(error=str(e)[-400:])
 
 
@@ -610,10 +746,16 @@ def main():
     ap.add_argument("--profile-out", default=None, help="keep the rocprofv3 summaries (kernel stats, PMC) here")
     ap.add_argument("--inflight", type=int, default=0, help="frames in flight (contexts / streams); 0 = default")
     ap.add_argument("--no-js", action="store_true", help="skip the JS drop-in trace_frame() timing")
+    ap.add_argument("--deadline", type=float, default=420.0,
+                    help="seconds from start by which the JSON line is printed (phases after the timed frames "
+                         "shrink or are skipped to fit; a watchdog prints what exists 30 s after it)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
+    deadline = Deadline(args.deadline)
+    reporter = Reporter()
+    reporter.arm(deadline)
     if args.gpus < 1:
         fail("--gpus must be >= 1")
 
@@ -643,6 +785,13 @@ def main():
                               int(os.environ.get("LOCAL_RANK", "0")))
     if rank != 0:
         return
+    report(args, res, spec, scene, W, H, refmax, build_s, deadline, reporter)
+
+
+def report(args, res, spec, scene, W, H, refmax, build_s, deadline, reporter):
+    """Rank 0: the record of the timed frames first (the watchdog can print it from here on), then the
+    optional phases in order of importance — rocprofv3 roofline passes, the CPU baseline, the JS
+    drop-in frame — each bounded by what the deadline leaves."""
     tot, el, steps = res["tot"], res["elapsed"], args.steps
     n_gpus = res["n_gpus"]
     value = tot["segments"] * steps / el / 1e6
@@ -654,34 +803,6 @@ def main():
                     trace_kernels_ms_hip_events=res["kernel_ms"],
                     algorithmic_bytes_per_frame=algorithmic_bytes(tot, BYTES_KERNEL),
                     reference_equivalent_bytes_per_frame=algorithmic_bytes(tot, BYTES_REF))
-    if n_gpus == 1 and not args.no_profile:
-        dur, err = kernel_durations(args)
-        pmc, notes = pmc_counters(args) if dur else ({}, [])
-        if dur:
-            kr = kernel_rooflines(dur, pmc, tot)
-            roofline["kernels"] = kr
-            roofline["kernel_ms_rocprof_sum"] = round(sum(dur.values()), 4)
-            top = max(kr, key=lambda k: kr[k]["ms_per_frame"])
-            t = kr[top]
-            if "valu_issue_frac" in t or "hbm_frac" in t:
-                bound = t.get("binding_roof", "valu-issue")
-                if bound == "valu-issue":
-                    slots = t["valu_issue_cycles"] / ISSUE_CYC
-                    roofline.update(bound="valu-issue", achieved=round(slots / (t["ms_per_frame"] * 1e-3) / 1e9, 2),
-                                    peak=round(SIMDS * t["clock_ghz"] / ISSUE_CYC, 1), unit="G VALU issue slots/s",
-                                    frac=t["valu_issue_frac"])
-                else:
-                    roofline.update(bound="hbm", achieved=t["hbm_GBps"], peak=HBM_PEAK_GBS, unit="GB/s",
-                                    frac=t["hbm_frac"])
-                roofline.update(kernel=top, traffic=t.get("hbm_bytes"), lane_util=t.get("lane_util"),
-                                note="dominant kernel against the roof that binds it: VALU issue (f64 at 4 "
-                                     "cycles, others at 2 per wave64 instruction per SIMD, at the kernel's "
-                                     "measured clock); HBM traffic = 2*FETCH_SIZE + WRITE_SIZE per frame")
-        if err or notes:
-            roofline["profile_notes"] = [x for x in [err] + notes if x]
-
-    cpu = cpu_baseline(spec, scene, cam, cfg, args.cpu_budget) if args.cpu_budget > 0 and n_gpus == 1 else None
-    js = js_frame(args) if n_gpus == 1 and not args.no_js else None
     rec = {
         "metric": "Mrays/s (whole node) at %dx%d" % (W, H),
         "value": round(value, 3),
@@ -704,12 +825,56 @@ def main():
         "roofline": roofline,
         "serial": serial,
         "host_frame": res["host"],
-        "js_frame": js,
-        "cpu_baseline": cpu,
+        "js_frame": None,
+        "cpu_baseline": None,
         "exposure": res["exposure"],
         "mpixels_per_s": round(W * H * steps / el / 1e6, 3),
+        "wall": dict(deadline_s=args.deadline, timed_frames_done_s=round(time.monotonic() - _T_START, 1)),
     }
-    print(json.dumps(rec), flush=True)
+    reporter.set(rec)
+
+    cpu_reserve = (3 * args.cpu_budget + 20) if args.cpu_budget > 0 and n_gpus == 1 else 0.0
+    if n_gpus == 1 and not args.no_profile:
+        reporter.phase = "rocprofv3"
+        dur, err = kernel_durations(args, deadline, reserve_s=cpu_reserve)
+        pmc, notes = pmc_counters(args, deadline, reserve_s=cpu_reserve) if dur else ({}, [])
+        roofline = dict(roofline)
+        if dur:
+            kr = kernel_rooflines(dur, pmc, tot)
+            roofline["kernels"] = kr
+            roofline["kernel_ms_rocprof_sum"] = round(sum(dur.values()), 4)
+            top = max(kr, key=lambda k: kr[k]["ms_per_frame"])
+            t = kr[top]
+            if "valu_issue_frac" in t or "hbm_frac" in t:
+                bound = t.get("binding_roof", "valu-issue")
+                if bound == "valu-issue":
+                    slots = t["valu_issue_cycles"] / ISSUE_CYC
+                    roofline.update(bound="valu-issue", achieved=round(slots / (t["ms_per_frame"] * 1e-3) / 1e9, 2),
+                                    peak=round(SIMDS * t["clock_ghz"] / ISSUE_CYC, 1), unit="G VALU issue slots/s",
+                                    frac=t["valu_issue_frac"])
+                else:
+                    roofline.update(bound="hbm", achieved=t["hbm_GBps"], peak=HBM_PEAK_GBS, unit="GB/s",
+                                    frac=t["hbm_frac"])
+                roofline.update(kernel=top, traffic=t.get("hbm_bytes"), lane_util=t.get("lane_util"),
+                                note="dominant kernel against the roof that binds it: VALU issue (f64 at 4 "
+                                     "cycles, others at 2 per wave64 instruction per SIMD, at the kernel's "
+                                     "measured clock); HBM traffic = 2*FETCH_SIZE + WRITE_SIZE per frame")
+        if err or notes:
+            roofline["profile_notes"] = [x for x in [err] + notes if x]
+        roofline["rocprof_pass_wall_s"] = list(_PROF_WALL)
+        reporter.update("roofline", roofline)
+        reporter.update_wall("rocprof_done_s")
+
+    if args.cpu_budget > 0 and n_gpus == 1:
+        reporter.phase = "cpu_baseline"
+        reporter.update("cpu_baseline", cpu_baseline(spec, scene, cam, cfg, args.cpu_budget, deadline, reserve_s=5.0))
+        reporter.update_wall("cpu_baseline_done_s")
+    if n_gpus == 1 and not args.no_js:
+        reporter.phase = "js_frame"
+        reporter.update("js_frame", js_frame(args, deadline.slice(90.0)))
+        reporter.update_wall("js_frame_done_s")
+    reporter.update_wall("emitted_s")
+    reporter.emit()
 
 
 if __name__ == "__main__":

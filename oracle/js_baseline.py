@@ -11,7 +11,9 @@ run(dir, threads) runs node on it and returns the per-pixel results and the timi
 import json
 import os
 import shutil
+import signal
 import subprocess
+import tempfile
 
 import numpy as np
 
@@ -57,11 +59,26 @@ def run(out_dir, threads=1, repeat=1, timeout=600):
     node = node_binary()
     if node is None:
         raise RuntimeError("node not found")
-    p = subprocess.run([node, "--max-old-space-size=8192", SCRIPT, out_dir, "--threads", str(threads),
-                        "--repeat", str(repeat)], capture_output=True, text=True, timeout=timeout)
-    if p.returncode != 0:
-        raise RuntimeError("rt_path.js failed (%d): %s" % (p.returncode, p.stderr[-2000:]))
-    info = json.loads(p.stdout.strip().splitlines()[-1])
+    # own session, output in files: at the timeout the whole group is killed and nothing can hold a
+    # pipe open (bench.py bounds its total wall time with these limits)
+    with tempfile.TemporaryFile() as fo, tempfile.TemporaryFile() as fe:
+        p = subprocess.Popen([node, "--max-old-space-size=8192", SCRIPT, out_dir, "--threads", str(threads),
+                              "--repeat", str(repeat)], stdout=fo, stderr=fe, start_new_session=True)
+        try:
+            rc = p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait()
+            raise
+        fo.seek(0)
+        fe.seek(0)
+        stdout, stderr = fo.read().decode(errors="replace"), fe.read().decode(errors="replace")
+    if rc != 0:
+        raise RuntimeError("rt_path.js failed (%d): %s" % (rc, stderr[-2000:]))
+    info = json.loads(stdout.strip().splitlines()[-1])
     rd = lambda n, dt: np.fromfile(os.path.join(out_dir, "out_%s.bin" % n), dtype=dt)
     res = dict(rgb=rd("rgb", "<f4").reshape(-1, 3), hit_entity=rd("hit_entity", "<i4"),
                hit_node=rd("hit_node", "<i4"), segments=rd("segments", "<i4"), status=rd("status", "u1"))
