@@ -453,6 +453,8 @@ function trace_ray(sc, walker, start, dir0, start_node, start_sub, out) {
     const t = path_len * cfg.distance_attenuation_factor;
     const isl = 1.0 / (Number.EPSILON + t ** 2);
     col = [col[0] * isl, col[1] * isl, col[2] * isl];
+    out.rgb = col;
+    walker.set_pos_and_dir(refpoint, dir);          // :276 (can throw)
   }
   out.rgb = col;
   return out;

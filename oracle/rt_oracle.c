@@ -1327,6 +1327,9 @@ static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], ui
         double t = path * cfg->distance_attenuation_factor;
         double isl = 1.0 / (2.220446049250313e-16 + t * t);   /* (x)**2 == x*x (fdlibm pow special case) */
         for (int i = 0; i < 3; i++) col[i] = col[i] * isl;
+        /* walker.set_pos_and_dir(this.refpoint, this.dir) — :276.  The colour is final, but the re-seat
+         * runs node_at_pos / setup_cur_node, which throw like the seat at :254: the frame aborts */
+        if (orc_walker_set(wk, o, d, NULL, 0) < 0) ro->status = ST_FAULT;
     }
 out:
     ro->rgb[0] = col[0]; ro->rgb[1] = col[1]; ro->rgb[2] = col[2];

@@ -499,6 +499,22 @@ static int order_after(RtDevice &src, hipStream_t waiter)
     return RT_OK;
 }
 
+// A one-device frame on a caller's stream uses d's scratch buffers (directions, candidate lists,
+// queues, counters, fault flag): order it after everything queued on d.stream (a synchronous frame,
+// a debug call) and d.stream after it, so no entry point of the context overwrites them mid-frame.
+static int bridge_in(RtDevice &d, hipStream_t st)
+{
+    return st == d.stream ? RT_OK : order_after(d, st);
+}
+
+static int bridge_out(RtDevice &d, hipStream_t st)
+{
+    if (st == d.stream) return RT_OK;
+    HIP_TRY(hipEventRecord(d.sync, st));
+    HIP_TRY(hipStreamWaitEvent(d.stream, d.sync, 0));
+    return RT_OK;
+}
+
 // Outputs of a whole frame on dev[0] (each nullable but rgb).
 struct FrameOut {
     float *rgb;
@@ -909,9 +925,11 @@ extern "C" int rt_trace_frame_device(rt_ctx *c, const rt_camera_desc *cam, const
         RtLaunch L;
         if ((r = prepare(c, d0, cam, cfg, 0, 1, cam->height, 0, L)) != RT_OK) return r;
         L.rgb = d_rgb;
+        if ((r = bridge_in(d0, st)) != RT_OK) return r;
         HIP_TRY(hipMemsetAsync(d0.b_fault.p, 0, sizeof(int), st));
         hipEvent_t *ev = next_events(d0);
-        return rt_launch_frame(L, st, ev[0], ev[1]);
+        if ((r = rt_launch_frame(L, st, ev[0], ev[1])) != RT_OK) return r;
+        return bridge_out(d0, st);
     }
     const FrameOut o = {d_rgb, nullptr, nullptr, nullptr};
     return frame_multi(c, cam, cfg, o, st, false);
@@ -952,6 +970,7 @@ extern "C" int rt_trace_rows_device(rt_ctx *c, const rt_camera_desc *cam, const 
     if (!d_rgb && L.rows > 0) return rt_set_error(RT_E_INVALID, "rt_trace_rows_device: d_rgb is null");
     hipStream_t st = stream ? (hipStream_t)stream : d0.stream;
     L.rgb = (float *)d_rgb;
+    if ((r = bridge_in(d0, st)) != RT_OK) return r;
     HIP_TRY(hipMemsetAsync(d0.b_fault.p, 0, sizeof(int), st));
     if (stats) {
         HIP_TRY(hipMemsetAsync(d0.b_counters.p, 0, sizeof(unsigned long long) * CT_N, st));
@@ -959,6 +978,7 @@ extern "C" int rt_trace_rows_device(rt_ctx *c, const rt_camera_desc *cam, const 
     }
     hipEvent_t *ev = next_events(d0);
     if ((r = rt_launch_frame(L, st, ev[0], ev[1])) != RT_OK) return r;
+    if ((r = bridge_out(d0, st)) != RT_OK) return r;
     if (stats) {
         unsigned long long h[CT_N] = {};
         HIP_TRY(hipMemcpyAsync(h, d0.b_counters.p, sizeof h, hipMemcpyDeviceToHost, st));

@@ -186,6 +186,24 @@ __device__ int walker_set(const RtDevScene &S, Walker &w, const double o[3], con
     return walker_setup(S, w) < 0 ? -1 : 0;
 }
 
+// Whether walker.set_pos_and_dir(p, d) (no node) throws: node_at_pos's Octree.get, or
+// setup_cur_node's negate(undefined) for a point outside the root — walker_set without the walker.
+__device__ bool reseat_throws(const RtDevScene &S, const double p[3], const double d[3])
+{
+    int t = -1, oc = 0;
+    long long lv = 0;
+    const int r = node_at_pos(S, p, t, oc, lv);
+    if (r != 0) return r < 0;
+    const NodeDims rd = node_dims(S, 0);
+    BoxIsect bi;
+    if (!box_isect(rd.x + 0.5 * rd.s, rd.y + 0.5 * rd.s, rd.z + 0.5 * rd.s, 1 * rd.s, p, d, bi)) return false;
+    int fi;
+    if (bi.u1 >= 0) fi = bi.i1;
+    else if (bi.u2 >= 0) fi = bi.i2;
+    else return false;
+    return fi < 0;
+}
+
 // The exit half of Box.line_intersection (src/math/intersection.ts:150-204) for a walker slot:
 // u2 = the first minimum over exit faces of q/p and the emptiness check u1 > u2, bit-identical to
 // six IEEE divisions.  Exactly one face per axis is an exit face (isNegative(p) selects entering),
@@ -1098,6 +1116,9 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         const double t = path * cfg.distance_attenuation_factor;
         const double isl = 1.0 / (2.220446049250313e-16 + t * t);
         col0 = col0 * isl; col1 = col1 * isl; col2 = col2 * isl;
+        // walker.set_pos_and_dir(this.refpoint, this.dir) — :276: no effect on the colour, but its
+        // node_at_pos / setup_cur_node throw like the seat at :254 (the frame aborts there)
+        if (walker_set(S, w, o, d, false, 0, 0, c) < 0) R.status = ST_FAULT;
     }
 done:
     R.rgb[0] = col0; R.rgb[1] = col1; R.rgb[2] = col2;
@@ -1610,6 +1631,8 @@ __device__ __forceinline__ bool early_shade(const RtLaunch &L, const RaySrc &src
     if (sh.image) return false;
     double c0 = 1.0 * sh.rgb[0], c1 = 1.0 * sh.rgb[1], c2 = 1.0 * sh.rgb[2];
     if (sh.light) {
+        // the post-light re-seat (src/raytracer.ts:276) may throw: then k_shade traces the ray
+        if (reseat_throws(S, h.p, src.d)) return false;
         const double a = h.p[0] - src.o[0], b = h.p[1] - src.o[1], e = h.p[2] - src.o[2];
         double path = 0;
         path += sqrt(dot3(a, b, e, a, b, e));

@@ -971,11 +971,14 @@ int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, 
     if (r != RT_OK) return r;
     const double validate_ms = ms_since(t0);
     r = 1;
+    // no frame may read the scene while it changes: a frame from rt_trace_frame_device /
+    // rt_trace_rows_device may still run on a caller stream, and a full upload overwrites the
+    // resident arrays in place, as an update patches them
+    for (int k = 0; k < st->ndev; k++) {
+        HIP_TRY(hipSetDevice(st->devs[k]));
+        HIP_TRY(hipDeviceSynchronize());
+    }
     if (incremental) {
-        for (int k = 0; k < st->ndev; k++) {        // no frame may read the scene while it changes
-            HIP_TRY(hipSetDevice(st->devs[k]));
-            HIP_TRY(hipDeviceSynchronize());
-        }
         r = st->update(s, oct, us);
         if (r < 0) return r;
     }

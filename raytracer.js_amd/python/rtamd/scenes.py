@@ -319,6 +319,33 @@ def make_config(refmax, sky=SKY_RGB, atten=1.0, default_substance=SUB_AIR, col_w
     return c
 
 
+def reseat_throw_scene(textured=False, width=64, height=48):
+    """A light whose hit point makes the post-light re-seat throw (src/raytracer.ts:276).
+
+    Non-dyadic root [-2, 1)^3 (size 3).  The light is a box in the root's Set whose +x face is at
+    x = 1 - 2^-53; the camera sits outside the root at (1.5, 0.5, 0.5) looking down -x, so the walker
+    returns only the root (src/octree_space.ts:254-277, 283-286) and rays hit the light's +x face.
+    There node_at_pos computes (x + 2)·(2/3) = 2 (rounded) and y, z in the upper halves: Octree.get(8)
+    throws.  The centre ray misses the light and hits a matte sphere, so the scan's first throw comes
+    after some pixels are final.  Returns (spec, camera)."""
+    e = _entities(2)
+    e["type"] = (abi.RT_ENT_BOX, abi.RT_ENT_SPHERE)
+    e["geom"][0, :4] = (0.8999999999999998, 0.8, 0.5, 0.2)
+    e["geom"][1, :4] = (0.2, 0.2, 0.6, 0.3)
+    e["shade"] = 0, 1
+    e["max_in_depth"], e["max_out_depth"] = 0, 0
+    sh = np.concatenate([_shade(light=1, rgb=(5, 4, 3)), _shade(rgb=(0.3, 0.6, 0.9))])
+    images = []
+    if textured:
+        sh["image"][0] = 1
+        images = [test_image(5, 3, 11)]
+    spec = SceneSpec("reseat_throw" + ("_tex" if textured else ""), e, sh, root_pos=(-2.0, -2.0, -2.0),
+                     root_size=3.0, images=images)
+    cam = make_camera(width, height, pos=(1.5, 0.5, 0.5), init_h=None, init_v=None)
+    cam.fr[:], cam.lf[:], cam.up[:] = [-1.0, 0.0, 0.0], [0.0, -1.0, 0.0], [0.0, 0.0, 1.0]
+    return spec, cam
+
+
 # Workloads named in BASELINE.json configs: (scene factory, width, height, refmax)
 WORKLOADS = {
     "config1": (config1_spheres, 256, 256, 2),

@@ -502,3 +502,36 @@ def test_hinted_level_grids_and_refill_config5(ctx):
     first = ctx.trace_frame(cam, cfg, stats=False, allow_fault=True)
     for _ in range(2):
         _same_frames(first, ctx.trace_frame(cam, cfg, stats=False, allow_fault=True))
+
+
+@pytest.mark.parametrize("textured", [False, True])
+def test_post_light_reseat_throws_like_the_reference(ctx, textured):
+    """src/raytracer.ts:276: after a light hit, Ray.trace re-seats the walker at the hit point.  On
+    this non-dyadic root the re-seat's node_at_pos computes Octree.get(8) and throws
+    (scenes.reseat_throw_scene), so the reference's trace_frame aborts at the first such pixel.  The
+    GPU frame equals the oracle's aborted frame bit for bit, the per-pixel status marks every such
+    light hit a fault, and the stats (fused) path agrees, counters included.  Untextured lights end
+    in the first-hit pass (early_shade), textured ones in k_shade's trace_ray."""
+    spec, cam = scenes.reseat_throw_scene(textured)
+    W, H = cam.width, cam.height
+    cfg = scenes.make_config(2)
+    old = np.random.default_rng(9).random(W * H * 3, dtype=np.float32)
+    w, root = oracle.build_scene(spec)
+    try:
+        full = w.trace_frame(root, cam, cfg)
+        want = w.trace_frame(root, cam, cfg, rgb=old.copy(), abort=True)
+    finally:
+        w.close()
+    light = full["hit_entity"] == 0
+    assert (full["status"][light] == 2).sum() > 100 and (full["status"][light] == 0).any()
+    assert full["status"][(H // 2) * W + W // 2] == 0          # the scan's first pixels are final
+    ctx.upload(rtamd.build_scene(spec))
+    got = ctx.trace_frame(cam, cfg, rgb=old.copy(), stats=False, allow_fault=True)
+    assert got["rc"] == abi.RT_E_FAULT
+    assert np.array_equal(got["rgb"].view(np.uint32), want["rgb"].view(np.uint32))
+    assert not np.array_equal(got["rgb"].view(np.uint32), old.view(np.uint32))
+    for k in ("hit_entity", "hit_node", "status"):
+        assert np.array_equal(got[k], full[k]), k
+    st = ctx.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True)
+    _same_frames(got, st)
+    assert st["stats"].counters() == full["counters"]

@@ -23,8 +23,8 @@ def _transmission_spec():
     return scenes.SceneSpec("transmission", ents, sh)
 
 
-def _check(spec, W, H, refmax, pixels, tmp_path, threads=1):
-    cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
+def _check(spec, W, H, refmax, pixels, tmp_path, threads=1, cam=None):
+    cam, cfg = cam or scenes.make_camera(W, H), scenes.make_config(refmax)
     d = str(tmp_path / spec.name)
     js_baseline.export(rtamd.build_scene(spec), cam, cfg, pixels, d)
     info, got = js_baseline.run(d, threads=threads)
@@ -54,3 +54,13 @@ def test_js_workers_config3_sample(tmp_path):
     pix = np.sort(rng.choice(1920 * 1080, 400, replace=False))
     info, _ = _check(scenes.config3(), 1920, 1080, 2, pix, tmp_path, threads=3)
     assert info["threads"] == 3 and info["pixels"] == 400
+
+
+def test_js_restatement_post_light_reseat_throws(tmp_path):
+    """src/raytracer.ts:276: the walker re-seat after a light hit throws on this scene
+    in the JS restatement exactly where the C oracle marks the pixel a fault."""
+    spec, cam = scenes.reseat_throw_scene()
+    W, H = cam.width, cam.height
+    _, got = _check(spec, W, H, 2, np.arange(W * H), tmp_path, cam=cam)
+    light = got["hit_entity"] == 0
+    assert (got["status"][light] == 2).sum() > 100 and (got["status"][light] == 0).any()

@@ -319,3 +319,33 @@ def test_builder_sync_new_nodes_shades_and_fallbacks():
     finally:
         ctx.close()
         p.close()
+
+
+@pytest.mark.gpu
+def test_full_sync_waits_for_a_frame_in_flight():
+    """A full upload (here: the first rt_builder_sync after rt_upload_scene) overwrites the resident
+    scene arrays in place.  A frame launched just before it with rt_trace_frame_device on a caller
+    stream must still see the old scene: the upload synchronises the context's devices first."""
+    import torch
+    old_spec, new_spec = scenes.config2(), scenes.small_random(3)
+    cam, cfg = scenes.make_camera(1920, 1080), scenes.make_config(1)
+    ctx = rtamd.Context(0)
+    b = rtamd.Builder.from_spec(new_spec)
+    try:
+        ctx.upload(rtamd.build_scene(old_spec))
+        s = torch.cuda.Stream()
+        want = torch.zeros((1080, 1920, 3), dtype=torch.float32, device="cuda")
+        ctx.trace_frame_device(cam, cfg, want.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        for _ in range(3):
+            got = torch.zeros_like(want)
+            torch.cuda.synchronize()
+            ctx.trace_frame_device(cam, cfg, got.data_ptr(), s.cuda_stream)   # in flight ...
+            st = ctx.sync(b)                                                   # ... while the scene changes
+            s.synchronize()
+            assert st.full == 1
+            assert torch.equal(got.view(torch.int32), want.view(torch.int32))
+            ctx.upload(rtamd.build_scene(old_spec))                            # back for the next round
+    finally:
+        ctx.close()
+        b.close()
