@@ -36,11 +36,13 @@ struct alignas(128) RtNode {
     int32_t child[8];       // child slot per octant, -1 = empty
     RtBvh box;              // copy of the cull-hierarchy root record (lo/hi); unused when n_ent == 0
     int32_t n_ent;          // EntitySet size
-    int32_t up_tree;        // parent slot (-1: root) — step_back
-    int32_t up_oct;         // index_within_parent (RT_OCT_UNDEF for the root, RT_OCT_BAD if not 0..7)
     int32_t ent_begin;      // first prim slot of the node's region (node_ent.x)
     int32_t bvh_root;       // cull-hierarchy root (node_ent.z, -1 without entities)
-    int32_t pad_[3];
+    int32_t pad_;
+    int32_t up_tree;        // parent slot (-1: root) — step_back
+    int32_t up_oct;         // index_within_parent (RT_OCT_UNDEF for the root, RT_OCT_BAD if not 0..7)
+    int32_t up2_tree;       // the parent's up_tree / up_oct (-1 / RT_OCT_UNDEF without a parent): the
+    int32_t up2_oct;        // walk climbs two levels without a load
 };
 static_assert(sizeof(RtNode) == 128, "RtNode must stay 128 bytes");
 

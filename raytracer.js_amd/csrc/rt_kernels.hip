@@ -409,92 +409,219 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
 // longer pay for two copies of the move and two cube loads per trip.  The slot's
 // parent link is read with its child id (one line), so a step_back does not wait for a load.
 // One trip of walker_run for this lane: nothing unless res == 1 (walking); sets res to the walk's end.
-template <bool STOP, bool ALL_FAST, typename Emit>
-__device__ __forceinline__ void walker_trip(const RtDevScene &S, Walker &w, Emit &&emit, int stop, int &res)
+// A trip is the head (trip_head: the slot's child id and parent link, the emit of a node returned on
+// entry, and the classification of the lane's next action), then the action (trip_step).
+enum : int { A_NONE = 0, A_STEPIN = 1, A_EXIT = 2, A_MOVE = 3 };
+#ifndef RT_CLIMB
+#define RT_CLIMB 2
+#endif
+#ifndef RT_PEEK
+#define RT_PEEK 1
+#endif
+
+template <bool STOP, typename Emit>
+__device__ __forceinline__ void trip_head(const RtDevScene &S, Walker &w, Emit &&emit, int stop, int &res, int &act,
+                                          int &lnode, int4 &up)
 {
-    enum : int { A_NONE = 0, A_STEPIN = 1, A_EXIT = 2, A_MOVE = 3 };
-    {
-        int act = A_NONE, lnode = -1;
-        int2 up = make_int2(-1, RT_OCT_UNDEF);
+    act = A_NONE;
+    lnode = -1;
+    up = make_int4(-1, RT_OCT_UNDEF, -1, RT_OCT_UNDEF);
+    if (res != 1) return;
+    const int ltree = w.cur_tree, loct = w.cur_oct;
+    if (++w.steps > STEP_CAP) {
+        res = -2;
+    } else if (loct != RT_OCT_UNDEF && (unsigned)loct > 7u) {
+        res = -1;                                          // Octree.get: index out of range
+    } else {
+        if (loct != RT_OCT_UNDEF) {
+            const RtNode &tn = S.node[ltree];
+            lnode = tn.child[loct];
+#if RT_CLIMB >= 2
+            up = *reinterpret_cast<const int4 *>(&tn.up_tree);   // parent and grandparent links, same line
+#else
+            up = make_int4(tn.up_tree, tn.up_oct, -1, RT_OCT_UNDEF);
+#endif
+        } else {
+            lnode = ltree;
+        }
+        if (!(w.flags & F_RET) && lnode >= 0) {
+            w.flags |= F_RET;
+            emit(lnode);
+            if (++w.steps > STEP_CAP) res = -2;            // the next call's first iteration
+        }
         if (res == 1) {
-            const int ltree = w.cur_tree, loct = w.cur_oct;
-            if (++w.steps > STEP_CAP) {
-                res = -2;
-            } else if (loct != RT_OCT_UNDEF && (unsigned)loct > 7u) {
-                res = -1;                                          // Octree.get: index out of range
-            } else {
-                if (loct != RT_OCT_UNDEF) {
-                    const RtNode &tn = S.node[ltree];
-                    lnode = tn.child[loct];
-                    up = make_int2(tn.up_tree, tn.up_oct);        // step_back's parent link, same line
-                } else {
-                    lnode = ltree;
-                }
-                if (!(w.flags & F_RET) && lnode >= 0) {
-                    w.flags |= F_RET;
-                    emit(lnode);
-                    if (++w.steps > STEP_CAP) res = -2;            // the next call's first iteration
-                }
-                if (res == 1) {
-                    if (loct == RT_OCT_UNDEF) res = 0;             // step_back from the tree's own slot
-                    else if (w.flags & F_AHEAD) act = A_MOVE;      // next_pos stands; the same normal again
-                    else if (!(w.flags & F_STEPPED) && lnode >= 0) act = A_STEPIN;
-                    else if (STOP && lnode < 0 && ltree * 8 + loct == stop) res = 2;
-                    else act = A_EXIT;
+            if (loct == RT_OCT_UNDEF) res = 0;             // step_back from the tree's own slot
+            else if (w.flags & F_AHEAD) act = A_MOVE;      // next_pos stands; the same normal again
+            else if (!(w.flags & F_STEPPED) && lnode >= 0) act = A_STEPIN;
+            else if (STOP && lnode < 0 && ltree * 8 + loct == stop) res = 2;
+            else act = A_EXIT;
+        }
+    }
+}
+
+// The lane's classified action: a step-in, or a slot exit falling through into the move along
+// next_pos's normal, or the move alone.  `act` is A_NONE afterwards.
+template <bool STOP, bool ALL_FAST>
+__device__ __forceinline__ void trip_step(const RtDevScene &S, Walker &w, int &res, int &act, int lnode, int4 &up,
+                                          int stop)
+{
+    if (act == A_STEPIN || act == A_EXIT) {
+        const NodeDims cd = node_dims(S, act == A_STEPIN ? lnode : w.cur_tree);
+        if (act == A_STEPIN) {
+            // octant_adj_pos(node, next_pos[0]) — :41-50, then step_in — :310-314
+            const double h = cd.s / 2;
+            const int px = w.np[0] >= cd.x + h, py = w.np[1] >= cd.y + h, pz = w.np[2] >= cd.z + h;
+            const int oct = (pz << 2) | (py << 1) | px;
+            w.depth++;
+            w.cur_tree = lnode;
+            w.cur_oct = oct;
+            w.flags &= ~F_RET;
+            act = A_NONE;
+#if RT_PEEK
+            // The next iteration at the entered slot, from the line whose cube was
+            // just read: an empty slot (not a segment's stop cell) is not returned and goes to its
+            // exit, whose cube is this one: take that iteration now, with its step.  A node in the
+            // slot is left to the next trip's head.
+            if (w.steps < STEP_CAP) {
+                const RtNode &tn = S.node[lnode];
+                if (tn.child[oct] < 0 && !(STOP && lnode * 8 + oct == stop)) {
+                    w.steps++;
+#if RT_CLIMB >= 2
+                    up = *reinterpret_cast<const int4 *>(&tn.up_tree);
+#else
+                    up = make_int4(tn.up_tree, tn.up_oct, -1, RT_OCT_UNDEF);
+#endif
+                    act = A_EXIT;
                 }
             }
+#endif
         }
-        if (act == A_STEPIN || act == A_EXIT) {
-            const NodeDims cd = node_dims(S, act == A_STEPIN ? lnode : w.cur_tree);
-            if (act == A_STEPIN) {
-                // octant_adj_pos(node, next_pos[0]) — :41-50, then step_in — :310-314
-                const double h = cd.s / 2;
-                const int px = w.np[0] >= cd.x + h, py = w.np[1] >= cd.y + h, pz = w.np[2] >= cd.z + h;
-                w.depth++;
-                w.cur_tree = lnode;
-                w.cur_oct = (pz << 2) | (py << 1) | px;
-                w.flags &= ~F_RET;
-            } else {
-                Counters c_unused;
-                if (walker_update_next_pos<ALL_FAST>(cd, w, c_unused) < 0) res = -1;
-                else act = A_MOVE;
-            }
+        if (act == A_EXIT) {
+            Counters c_unused;
+            if (walker_update_next_pos<ALL_FAST>(cd, w, c_unused) < 0) { res = -1; act = A_NONE; }
+            else act = A_MOVE;
         }
-        if (act == A_MOVE) {
-            const int loct = w.cur_oct;
-            if (!(w.nn & 16)) {
-                res = -1;                                          // vector.add(v, undefined)
+    }
+    if (act == A_MOVE) {
+        act = A_NONE;
+        const int loct = w.cur_oct;
+        if (!(w.nn & 16)) {
+            res = -1;                                          // vector.add(v, undefined)
+        } else {
+            const int face = w.nn & 7, axis = face >> 1;
+            int delta = (face & 1) ? 1 : -1;
+            if (w.nn & 8) delta = -delta;
+            const int nb = ((loct >> axis) & 1) + delta;
+            if (nb >= 0 && nb <= 1) {
+                w.cur_oct = (loct & ~(1 << axis)) | (nb << axis);
+                w.flags = 0;
             } else {
-                const int face = w.nn & 7, axis = face >> 1;
-                int delta = (face & 1) ? 1 : -1;
-                if (w.nn & 8) delta = -delta;
-                const int nb = ((loct >> axis) & 1) + delta;
-                if (nb >= 0 && nb <= 1) {
-                    w.cur_oct = (loct & ~(1 << axis)) | (nb << axis);
-                    w.flags = 0;
-                } else {
-                    w.flags |= F_AHEAD | F_STEPPED;                // step_back — :280-308
-                    if (w.depth > 0) { w.depth--; w.flags |= F_RET; }
-                    else w.flags &= ~F_RET;
-                    if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
-                    else w.cur_oct = RT_OCT_UNDEF;
+                w.flags |= F_AHEAD | F_STEPPED;                // step_back — :280-308
+                const bool deep = w.depth > 0;
+                if (deep) { w.depth--; w.flags |= F_RET; }
+                else w.flags &= ~F_RET;
+                if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
+                else w.cur_oct = RT_OCT_UNDEF;
+#if RT_CLIMB
+                // The next iteration at the parent slot: its child is the node just
+                // left (already returned: F_RET, depth was > 0), F_AHEAD moves it along the same normal
+                // again.  When that move is a sibling move it needs no load: do it now, with its step.
+                // Otherwise (another step_back, a bad or undefined octant, the step cap) the next trip's
+                // head takes the parent slot as before.
+                if (deep && up.x >= 0 && (unsigned)up.y <= 7u && w.steps < STEP_CAP) {
+                    const int nb2 = ((up.y >> axis) & 1) + delta;
+                    if (nb2 >= 0 && nb2 <= 1) {
+                        w.steps++;
+                        w.cur_oct = (up.y & ~(1 << axis)) | (nb2 << axis);
+                        w.flags = 0;
+                    }
+#if RT_CLIMB >= 2
+                    else {
+                        // that move is a step_back too: with the grandparent link (up.z, up.w) of the
+                        // same record, take it, and the grandparent slot's sibling move when it is one
+                        w.steps++;                                 // the parent slot's iteration
+                        const bool deep2 = w.depth > 0;
+                        if (deep2) w.depth--;
+                        else w.flags &= ~F_RET;
+                        if (up.z >= 0) { w.cur_tree = up.z; w.cur_oct = up.w; }
+                        else w.cur_oct = RT_OCT_UNDEF;
+                        const int nb3 = ((up.w >> axis) & 1) + delta;
+                        if (deep2 && up.z >= 0 && (unsigned)up.w <= 7u && nb3 >= 0 && nb3 <= 1 && w.steps < STEP_CAP) {
+                            w.steps++;
+                            w.cur_oct = (up.w & ~(1 << axis)) | (nb3 << axis);
+                            w.flags = 0;
+                        }
+                    }
+#endif
                 }
+#endif
             }
         }
     }
 }
 
+template <bool STOP, bool ALL_FAST, typename Emit>
+__device__ __forceinline__ void walker_trip(const RtDevScene &S, Walker &w, Emit &&emit, int stop, int &res)
+{
+    int act, lnode;
+    int4 up;
+    trip_head<STOP>(S, w, emit, stop, res, act, lnode, up);
+    trip_step<STOP, ALL_FAST>(S, w, res, act, lnode, up, stop);
+}
+
 #ifndef RT_TRIP_UNROLL
 #define RT_TRIP_UNROLL 1
 #endif
+#ifndef RT_WALK_PROF
+#define RT_WALK_PROF 0
+#endif
+#if RT_WALK_PROF
+// Diagnostic build (-DRT_WALK_PROF=1, tools/walk_profile.py): per walk loop, wave-level executions and
+// active lanes of each part of a trip, summed over the frame.  [0] trips, [1] walking lanes at trip
+// start, [2] head executions, [3] head lanes, [4] emit executions, [5] emit lanes, [6] step-in
+// executions, [7] step-in lanes, [8] exit executions, [9] exit lanes, [10] move executions, [11] move
+// lanes (exits included), [12] walks (lanes), [13] waves.
+__device__ unsigned long long g_walk_prof[16];
+struct WalkProf {
+    unsigned long long v[14] = {};
+    __device__ void add(int i, unsigned long long m) { if (m) { v[i] += 1; v[i + 1] += __popcll(m); } }
+    __device__ void flush()
+    {
+        if ((threadIdx.x & 63) == 0)
+            for (int i = 0; i < 14; i++) if (v[i]) atomicAdd(&g_walk_prof[i], v[i]);
+    }
+};
+#endif
+
 template <bool STOP, bool ALL_FAST, typename Emit>
 __device__ __forceinline__ int walker_run_t(const RtDevScene &S, Walker &w, Emit &&emit, int stop)
 {
     int res = w.cur_tree >= 0 ? 1 : 0;
+#if RT_WALK_PROF
+    WalkProf pf;
+    pf.v[12] = __popcll(__ballot(res == 1));
+    pf.v[13] = 1;
+    do {
+        int act, lnode;
+        int4 up;
+        const unsigned long long mw = __ballot(res == 1);
+        pf.add(0, mw);
+        pf.add(2, mw);
+        const int f0 = w.flags;
+        trip_head<STOP>(S, w, emit, stop, res, act, lnode, up);
+        pf.add(4, __ballot(((w.flags & ~f0) & F_RET) && ((mw >> (threadIdx.x & 63)) & 1)));
+        pf.add(6, __ballot(act == A_STEPIN));
+        pf.add(8, __ballot(act == A_EXIT));
+        pf.add(10, __ballot(act == A_EXIT || act == A_MOVE));
+        trip_step<STOP, ALL_FAST>(S, w, res, act, lnode, up, stop);
+    } while (__ballot(res == 1));
+    pf.flush();
+#else
     do {
 #pragma unroll
         for (int u = 0; u < RT_TRIP_UNROLL; u++) walker_trip<STOP, ALL_FAST>(S, w, emit, stop, res);
     } while (__ballot(res == 1));
+#endif
     return res;
 }
 
@@ -1927,4 +2054,22 @@ int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[
                            max_out, d_tree, d_oct, d_n);
     HIP_TRY(hipGetLastError());
     return RT_OK;
+}
+
+// RT_WALK_PROF builds: read (and optionally clear) the walk-loop profile (tools/walk_profile.py).
+extern "C" int rt_debug_walk_profile(unsigned long long *out16, int reset)
+{
+#if RT_WALK_PROF
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_walk_prof), sizeof(unsigned long long) * 16) != hipSuccess)
+        return RT_E_HIP;
+    if (reset) {
+        static const unsigned long long zero[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_walk_prof), zero, sizeof zero) != hipSuccess) return RT_E_HIP;
+    }
+    return RT_OK;
+#else
+    (void)out16;
+    (void)reset;
+    return RT_E_UNSUPPORTED;
+#endif
 }

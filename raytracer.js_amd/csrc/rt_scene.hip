@@ -264,6 +264,12 @@ struct RtSceneStore {
     // host mirrors of the device arrays (the diff base)
     std::vector<RtNode> m_node;                        // 1 / slot
     std::vector<int32_t> m_up, m_ent, m_dfs;           // 2, 4, 1 / slot
+    // a node record's grandparent link: its parent's {up_tree, up_oct} (the parent's m_up is set first)
+    void set_up2(RtNode &nd) const
+    {
+        nd.up2_tree = nd.up_tree >= 0 ? m_up[2 * (size_t)nd.up_tree] : -1;
+        nd.up2_oct = nd.up_tree >= 0 ? m_up[2 * (size_t)nd.up_tree + 1] : RT_OCT_UNDEF;
+    }
     std::vector<int32_t> m_order;                      // slot of each DFS id
     std::vector<int32_t> m_list;                       // 1 / list-pool entry
     std::vector<int32_t> m_type, m_shade, m_sub;       // 1 / entity
@@ -520,6 +526,7 @@ struct RtSceneStore {
             m_up[2 * n + 1] = oct[n];
             nd.up_tree = m_up[2 * n];
             nd.up_oct = oct[n];
+            set_up2(nd);
             m_dfs[n] = n;
             m_order[n] = n;
             slot_of.emplace(node_key(s, n), n);
@@ -730,6 +737,7 @@ struct RtSceneStore {
             m_up[2 * (size_t)sl + 1] = oct[n];
             nd.up_tree = m_up[2 * (size_t)sl];
             nd.up_oct = oct[n];
+            set_up2(nd);
             if (n > 0 && slot_of_dfs[s->node_parent[n]] < (int)n_old) touched.push_back(slot_of_dfs[s->node_parent[n]]);
             slot_of.emplace(node_key(s, n), sl);
         }
@@ -880,6 +888,7 @@ struct RtSceneStore {
             nd.up_tree = m_up[2 * (size_t)sl] = e.rec_up[2 * k];
             nd.up_oct = m_up[2 * (size_t)sl + 1] = e.rec_up[2 * k + 1];
         }
+        for (size_t k = 0; k < e.rec_slot.size(); k++) set_up2(m_node[e.rec_slot[k]]);   // parents may be new too
         add_slots(A_NODE_UP, e.rec_slot, m_up.data(), 2 * sizeof(int32_t));
         std::vector<int32_t> ent_slots(e.set_slot);
         std::sort(ent_slots.begin(), ent_slots.end());

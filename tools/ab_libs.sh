@@ -11,7 +11,7 @@ for E in ${LIBS:-cur=}; do
   if [ -n "$P" ]; then export RT_LIB=$PWD/$P; else unset RT_LIB; fi
   rm -rf "$OUT/$L"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/$L" -o kt --output-format csv -- \
-      python3 tools/sweep.py --frames $FR ${SWEEP:-base:} > "$OUT/$L.log" 2>&1 || { echo "$L failed"; tail -5 "$OUT/$L.log"; exit 1; }
+      python3 tools/sweep.py --frames $FR ${SWEEP_ARGS:-} ${SWEEP:-base:} > "$OUT/$L.log" 2>&1 || { echo "$L failed"; tail -5 "$OUT/$L.log"; exit 1; }
   python3 - "$OUT/$L" $((FR + 3)) $L <<'PY'
 import csv, glob, sys, re
 d, frames, tag = sys.argv[1], int(sys.argv[2]), sys.argv[3]
