@@ -84,6 +84,8 @@ struct RtDevScene {
     const RtImage *images;      // [n_images] ImageTextures: texel bytes at texels + offset
     const uint8_t *texels;
     int32_t n_nodes, n_list, n_entities, n_shades, n_subs, n_bvh, n_images;
+    int32_t exact_slots;        // every node's slot planes equal its slot positions (dyadic cubes): the
+                                // walker takes them without recomputing the Box centre (rt_kernels.hip)
 };
 
 // A ray of the split path at its first continuation (segment start after a mirror / transmission

@@ -212,25 +212,24 @@ __device__ bool reseat_throws(const RtDevScene &S, const double p[3], const doub
 // where both are +-inf or NaN).  Any candidate farther than 8 ulps from the minimum cannot be
 // (or tie with) the exact minimum, so only the survivors are divided exactly — normally one.
 // Returns false for the reference's [] (then update_next_pos throws).
-__device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, double size, const Walker &w,
-                                          double &u2o, int &i2o)
+// The slot is given by its planes: tl[a] = the Box's `center - size*0.5` per axis (its lower face),
+// top[a] = `tl + size` (its upper face), computed with the reference's operations by the caller.
+__device__ __forceinline__ bool slot_exit(const double tl[3], const double top[3], const Walker &w, double &u2o,
+                                          int &i2o)
 {
-    const double hs = size * 0.5;
-    const double c[3] = {cx, cy, cz};
-    // face 2a: p = -d, face 2a+1: p = d; isNegative(p) picks the entering one.  Only the screening
-    // products are kept; the one (normally) surviving quotient is recomputed from its axis below,
-    // with the same operations, so the live state stays small (the walker runs at 4+ waves/SIMD).
-    double ae[3];
+    // face 2a: p = -d, face 2a+1: p = d; isNegative(p) picks the entering one.  qe = the exit face's
+    // q, kept for the division; the entry face's only feeds the screen (and the rare exact check)
+    double ae[3], qe[3];
     double M = -INFINITY;                                // entry: u1 = first strict maximum
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        const double tl = c[a] - hs;
-        const double qlo = w.o[a] - tl;
-        const double qhi = tl + size - w.o[a];
+        const double qlo = w.o[a] - tl[a];
+        const double qhi = top[a] - w.o[a];
         const bool neg = signbit(w.d[a]);
         // (neg ? -inv : inv) is |inv| (inv = RN(1/d) has d's sign; a NaN quotient never survives):
         // the abs / neg source modifiers of the multiply, no per-ray register copies
-        ae[a] = (neg ? qlo : qhi) * fabs(w.inv[a]);
+        qe[a] = neg ? qlo : qhi;
+        ae[a] = qe[a] * fabs(w.inv[a]);
         const double an = (neg ? qhi : qlo) * -fabs(w.inv[a]);
         M = an > M ? an : M;
     }
@@ -247,13 +246,10 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
     int i2;
     {
         const int k = s0 ? 0 : (s1 ? 1 : 2);
-        const double ck = s0 ? cx : (s1 ? cy : cz), ok = s0 ? w.o[0] : (s1 ? w.o[1] : w.o[2]);
+        const double q = s0 ? qe[0] : (s1 ? qe[1] : qe[2]);
         const double dk = s0 ? w.d[0] : (s1 ? w.d[1] : w.d[2]);
-        const double tl = ck - hs;
-        const bool neg = signbit(dk);
-        const double q = neg ? ok - tl : tl + size - ok;
         u2 = q / fabs(dk);                                   // (neg ? -d : d), bit for bit unless NaN
-        i2 = 2 * k + (neg ? 0 : 1);
+        i2 = 2 * k + (signbit(dk) ? 0 : 1);
     }
     if (!(u2 < INFINITY)) { u2 = INFINITY; i2 = -1; }          // (a finite survivor never gets here)
     if (!common) {
@@ -265,10 +261,8 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
 #pragma unroll
             for (int a = 0; a < 3; a++) {
                 if (all || ae[a] <= m + tol) {
-                    const double tl = c[a] - hs;
-                    const bool neg = signbit(w.d[a]);
-                    const double e = (neg ? w.o[a] - tl : tl + size - w.o[a]) / fabs(w.d[a]);
-                    if (e < u2) { u2 = e; i2 = neg ? 2 * a : 2 * a + 1; }
+                    const double e = qe[a] / fabs(w.d[a]);
+                    if (e < u2) { u2 = e; i2 = signbit(w.d[a]) ? 2 * a : 2 * a + 1; }
                 }
             }
         }
@@ -279,9 +273,8 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
         double u1 = -INFINITY;
 #pragma unroll
         for (int a = 0; a < 3; a++) {
-            const double tl = c[a] - hs;
             const bool neg = signbit(w.d[a]);
-            const double e = (neg ? tl + size - w.o[a] : w.o[a] - tl) / -fabs(w.d[a]);
+            const double e = (neg ? top[a] - w.o[a] : w.o[a] - tl[a]) / -fabs(w.d[a]);
             if (e > u1) u1 = e;
         }
         if (u1 > u2) return false;
@@ -292,23 +285,42 @@ __device__ __forceinline__ bool slot_exit(double cx, double cy, double cz, doubl
 }
 
 // update_next_pos — :369-384 with dim_relative_to_parent :127-136.  Returns 0 or -1 (throw).
-// `p` = the cube of w.cur_tree.
+// `p` = the cube of w.cur_tree.  The slot's cube is dim_relative_to_parent's {p.pos + bit·(p.size/2),
+// p.size/2}, and its Box planes are tl = (pos + 0.5·size) − size·0.5 and tl + size.  `exact` (the
+// scene's RtDevScene::exact_slots, wave-uniform): every node's slots have tl == pos bit for bit
+// (dyadic cubes; checked at upload), so tl is the slot position itself.
 // ALL_FAST: the caller knows w.fast holds (walker_run's wave-uniform fast loop), so the exact
 // six-division path is not compiled in.
 template <bool ALL_FAST = false>
-__device__ __forceinline__ int walker_update_next_pos(const NodeDims &p, Walker &w, Counters &c)
+__device__ __forceinline__ int walker_update_next_pos(const NodeDims &p, Walker &w, Counters &c, bool exact)
 {
     c.slot++;
     const int n = w.cur_oct;
     const double ph = p.s / 2;
-    const double dx = p.x + (double)((n >> 0) & 1) * ph;
-    const double dy = p.y + (double)((n >> 1) & 1) * ph;
-    const double dz = p.z + (double)((n >> 2) & 1) * ph;
+    const double pc[3] = {p.x, p.y, p.z};
     double u2;
     int i2;
     if (ALL_FAST || w.fast) {
-        if (!slot_exit(dx + 0.5 * ph, dy + 0.5 * ph, dz + 0.5 * ph, 1 * ph, w, u2, i2)) return -1;
+        double tl[3], top[3];
+        if (exact) {
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                tl[a] = pc[a] + (((n >> a) & 1) ? ph : 0.0);      // (double)bit * ph is ph or +0
+                top[a] = tl[a] + ph;
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const double dx = pc[a] + (double)((n >> a) & 1) * ph;
+                tl[a] = (dx + 0.5 * ph) - ph * 0.5;
+                top[a] = tl[a] + ph;
+            }
+        }
+        if (!slot_exit(tl, top, w, u2, i2)) return -1;
     } else {
+        const double dx = p.x + (double)((n >> 0) & 1) * ph;
+        const double dy = p.y + (double)((n >> 1) & 1) * ph;
+        const double dz = p.z + (double)((n >> 2) & 1) * ph;
         BoxIsect bi;
         if (!box_isect(dx + 0.5 * ph, dy + 0.5 * ph, dz + 0.5 * ph, 1 * ph, w.o, w.d, bi)) return -1;
         u2 = bi.u2;
@@ -361,7 +373,7 @@ __device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_t
                     continue;
                 }
                 if (STOP && lnode < 0 && ltree * 8 + loct == stop) return 2;
-                if (walker_update_next_pos(node_dims(S, w.cur_tree), w, c) < 0) return -1;
+                if (walker_update_next_pos(node_dims(S, w.cur_tree), w, c, S.exact_slots != 0) < 0) return -1;
             }
             if (!(w.nn & 16)) return -1;                     // vector.add(v, undefined)
             // cur_octant + normal: only the normal's axis can leave {0,1}
@@ -498,7 +510,7 @@ __device__ __forceinline__ void trip_step(const RtDevScene &S, Walker &w, int &r
         }
         if (act == A_EXIT) {
             Counters c_unused;
-            if (walker_update_next_pos<ALL_FAST>(cd, w, c_unused) < 0) { res = -1; act = A_NONE; }
+            if (walker_update_next_pos<ALL_FAST>(cd, w, c_unused, S.exact_slots != 0) < 0) { res = -1; act = A_NONE; }
             else act = A_MOVE;
         }
     }

@@ -252,6 +252,23 @@ double ms_since(std::chrono::steady_clock::time_point t0)
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// Whether the walker may take a node's slot planes as the slot positions (RtDevScene::exact_slots):
+// for each axis and half, dim_relative_to_parent's pos = p + bit·(size/2) and the Box's lower plane
+// (pos + 0.5·h) − h·0.5 (src/octree_space.ts:127-136, src/math/intersection.ts:150-160) are the
+// same double, bit for bit (so signed zeros too).  Holds on dyadic cubes.
+static bool slot_planes_exact(const RtNode &nd)
+{
+    const double h = nd.s / 2;
+    const double p[3] = {nd.x, nd.y, nd.z};
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 2; b++) {
+            const double pos = p[a] + (double)b * h;
+            const double tl = (pos + 0.5 * h) - h * 0.5;
+            if (memcmp(&pos, &tl, sizeof pos) != 0) return false;
+        }
+    return true;
+}
+
 }  // namespace
 
 struct RtSceneStore {
@@ -264,6 +281,18 @@ struct RtSceneStore {
     // host mirrors of the device arrays (the diff base)
     std::vector<RtNode> m_node;                        // 1 / slot
     std::vector<int32_t> m_up, m_ent, m_dfs;           // 2, 4, 1 / slot
+    // Slots whose Box planes differ from their positions (walker_update_next_pos): per slot, and how
+    // many.  A node's cube never changes once written, except by a full upload, which recounts.
+    std::vector<uint8_t> m_inexact;
+    size_t n_inexact = 0;
+    void note_cube(size_t sl)
+    {
+        if (m_inexact.size() <= sl) m_inexact.resize(sl + 1, 0);
+        const uint8_t f = slot_planes_exact(m_node[sl]) ? 0 : 1;
+        n_inexact += f;
+        n_inexact -= m_inexact[sl];
+        m_inexact[sl] = f;
+    }
     // a node record's grandparent link: its parent's {up_tree, up_oct} (the parent's m_up is set first)
     void set_up2(RtNode &nd) const
     {
@@ -469,6 +498,11 @@ struct RtSceneStore {
         d.n_shades = n_shades;
         d.n_subs = n_subs;
         d.n_bvh = (int32_t)bvh_used;
+#ifdef RT_NO_EXACT_SLOTS
+        d.exact_slots = 0;                             // A/B builds: the general plane computation only
+#else
+        d.exact_slots = n_inexact == 0 ? 1 : 0;
+#endif
     }
 
     void entity_mirrors(const rt_scene_desc *s)
@@ -504,6 +538,8 @@ struct RtSceneStore {
         slot_of.clear();
         slot_of.reserve((size_t)N * 2);
         m_node.resize(N);
+        m_inexact.assign(N, 0);
+        n_inexact = 0;
         m_up.assign(2 * (size_t)N, 0);
         m_ent.assign(4 * (size_t)N, 0);
         m_dfs.resize(N);
@@ -527,6 +563,7 @@ struct RtSceneStore {
             nd.up_tree = m_up[2 * n];
             nd.up_oct = oct[n];
             set_up2(nd);
+            note_cube(n);
             m_dfs[n] = n;
             m_order[n] = n;
             slot_of.emplace(node_key(s, n), n);
@@ -738,6 +775,7 @@ struct RtSceneStore {
             nd.up_tree = m_up[2 * (size_t)sl];
             nd.up_oct = oct[n];
             set_up2(nd);
+            note_cube(sl);
             if (n > 0 && slot_of_dfs[s->node_parent[n]] < (int)n_old) touched.push_back(slot_of_dfs[s->node_parent[n]]);
             slot_of.emplace(node_key(s, n), sl);
         }
@@ -888,7 +926,10 @@ struct RtSceneStore {
             nd.up_tree = m_up[2 * (size_t)sl] = e.rec_up[2 * k];
             nd.up_oct = m_up[2 * (size_t)sl + 1] = e.rec_up[2 * k + 1];
         }
-        for (size_t k = 0; k < e.rec_slot.size(); k++) set_up2(m_node[e.rec_slot[k]]);   // parents may be new too
+        for (size_t k = 0; k < e.rec_slot.size(); k++) {        // parents may be new too
+            set_up2(m_node[e.rec_slot[k]]);
+            note_cube(e.rec_slot[k]);
+        }
         add_slots(A_NODE_UP, e.rec_slot, m_up.data(), 2 * sizeof(int32_t));
         std::vector<int32_t> ent_slots(e.set_slot);
         std::sort(ent_slots.begin(), ent_slots.end());
