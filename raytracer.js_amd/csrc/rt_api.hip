@@ -452,7 +452,8 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     if (c->split && P > 0) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).
-        L.cand_cap = c->cand_cap;
+        // the walk kernels address the lists with 32-bit byte offsets (cand_store): cand_cap * P * 4 < 2^32
+        L.cand_cap = (int32_t)std::min<long long>(c->cand_cap, ((1ll << 32) - 1) / (4ll * P));
         if (d.b_cand.ensure(sizeof(int32_t) * (size_t)L.cand_cap * P) == RT_OK &&
             d.b_cand_n.ensure(2 * sizeof(int32_t) * P) == RT_OK && d.b_first.ensure(2 * sizeof(int32_t) * P) == RT_OK &&
             d.b_queue.ensure(3 * sizeof(RtCont) * P) == RT_OK) {

@@ -1,6 +1,7 @@
 // rt_internal.h — shared between the C-ABI host code (rt_api.hip, rt_builder.cpp) and the kernels.
 #pragma once
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include <vector>
@@ -45,6 +46,9 @@ struct alignas(128) RtNode {
     int32_t up2_oct;        // walk climbs two levels without a load
 };
 static_assert(sizeof(RtNode) == 128, "RtNode must stay 128 bytes");
+static_assert(offsetof(RtNode, child) == 32 && offsetof(RtNode, box) == 64 && offsetof(RtNode, n_ent) == 96 &&
+                  offsetof(RtNode, up_tree) == 112 && offsetof(RtNode, up2_oct) == 124,
+              "RtNode field offsets are used by the kernels' 32-bit node addressing");
 
 // A loaded ImageTexture (rt_image_desc): width x height RGB bytes at texels + offset.
 struct RtImage {

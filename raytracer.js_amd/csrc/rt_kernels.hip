@@ -36,10 +36,45 @@ constexpr int STEP_CAP = 1 << 24;                // per-walk loop bound: every l
 // ---- node access --------------------------------------------------------------------------------
 struct NodeDims { double x, y, z, s; };
 
+// Node records are addressed as the array base (wave-uniform, SGPRs) plus a 32-bit byte offset, so a
+// load is one v_lshl_add_u32 and a saddr global load instead of 64-bit address arithmetic per access
+// (the node array is far below 4 GB: 128 B per node).
+template <typename T>
+__device__ __forceinline__ T ld_at(const void *base, uint32_t off)
+{
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + off);
+}
+__device__ __forceinline__ uint32_t node_off(int n) { return (uint32_t)n << 7; }
+enum : uint32_t { NODE_CHILD = 32, NODE_BOX = 64, NODE_NENT = 96, NODE_UP = 112 };
+
 __device__ __forceinline__ NodeDims node_dims(const RtDevScene &S, int n)
 {
-    const double4 v = *reinterpret_cast<const double4 *>(&S.node[n].x);
+    const double4 v = ld_at<double4>(S.node, node_off(n));
     return {v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ int node_child(const RtDevScene &S, int n, int oct)
+{
+    return ld_at<int32_t>(S.node, node_off(n) + NODE_CHILD + ((uint32_t)oct << 2));
+}
+
+// {up_tree, up_oct, up2_tree, up2_oct} of node n (one 16-byte load)
+__device__ __forceinline__ int4 node_up4(const RtDevScene &S, int n) { return ld_at<int4>(S.node, node_off(n) + NODE_UP); }
+
+// The walk pass's candidate filter of a returned node: it has entities and (culling on, finite ray)
+// the ray crosses its cull-hierarchy root box.  One line: count and box.
+struct RayBox;
+__device__ __forceinline__ bool node_candidate(const RtDevScene &S, int n, bool cull, const RayBox &rb);
+
+// Candidate lists are k-major [cand_cap][rays] int32; (k * stride + ray) * 4 < 2^32 is ensured by
+// the host (prepare caps cand_cap), so the store address is a 32-bit offset from the uniform base.
+__device__ __forceinline__ void cand_store(int32_t *cand, int k, uint32_t stride, uint32_t ray, int node)
+{
+    *reinterpret_cast<int32_t *>(reinterpret_cast<char *>(cand) + (((uint32_t)k * stride + ray) << 2)) = node;
+}
+__device__ __forceinline__ int cand_load(const int32_t *cand, int k, uint32_t stride, uint32_t ray)
+{
+    return ld_at<int32_t>(cand, ((uint32_t)k * stride + ray) << 2);
 }
 
 // ---- Box.line_intersection (src/math/intersection.ts:150-204) on a cube ----------------------------
@@ -446,12 +481,11 @@ __device__ __forceinline__ void trip_head(const RtDevScene &S, Walker &w, Emit &
         res = -1;                                          // Octree.get: index out of range
     } else {
         if (loct != RT_OCT_UNDEF) {
-            const RtNode &tn = S.node[ltree];
-            lnode = tn.child[loct];
-#if RT_CLIMB >= 2
-            up = *reinterpret_cast<const int4 *>(&tn.up_tree);   // parent and grandparent links, same line
-#else
-            up = make_int4(tn.up_tree, tn.up_oct, -1, RT_OCT_UNDEF);
+            lnode = node_child(S, ltree, loct);
+            up = node_up4(S, ltree);                       // parent and grandparent links, same line
+#if RT_CLIMB < 2
+            up.z = -1;
+            up.w = RT_OCT_UNDEF;
 #endif
         } else {
             lnode = ltree;
@@ -495,13 +529,12 @@ __device__ __forceinline__ void trip_step(const RtDevScene &S, Walker &w, int &r
             // exit, whose cube is this one: take that iteration now, with its step.  A node in the
             // slot is left to the next trip's head.
             if (w.steps < STEP_CAP) {
-                const RtNode &tn = S.node[lnode];
-                if (tn.child[oct] < 0 && !(STOP && lnode * 8 + oct == stop)) {
+                if (node_child(S, lnode, oct) < 0 && !(STOP && lnode * 8 + oct == stop)) {
                     w.steps++;
-#if RT_CLIMB >= 2
-                    up = *reinterpret_cast<const int4 *>(&tn.up_tree);
-#else
-                    up = make_int4(tn.up_tree, tn.up_oct, -1, RT_OCT_UNDEF);
+                    up = node_up4(S, lnode);
+#if RT_CLIMB < 2
+                    up.z = -1;
+                    up.w = RT_OCT_UNDEF;
 #endif
                     act = A_EXIT;
                 }
@@ -806,6 +839,19 @@ __device__ __forceinline__ bool ray_box(const RtBvh &b, const RayBox &rb)
     const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
     const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
     return tmin <= tmax;
+}
+
+__device__ __forceinline__ bool node_candidate(const RtDevScene &S, int n, bool cull, const RayBox &rb)
+{
+    const uint32_t off = node_off(n);
+    if (ld_at<int32_t>(S.node, off + NODE_NENT) == 0) return false;
+    if (!cull || !rb.ok) return true;
+    const float4 lo = ld_at<float4>(S.node, off + NODE_BOX);        // lo.xyz, hi.x
+    const float2 hi = ld_at<float2>(S.node, off + NODE_BOX + 16);   // hi.yz
+    RtBvh b;
+    b.lo[0] = lo.x; b.lo[1] = lo.y; b.lo[2] = lo.z;
+    b.hi[0] = lo.w; b.hi[1] = hi.x; b.hi[2] = hi.y;
+    return ray_box(b, rb);
 }
 
 // Entity.collision_info dispatch: 1 hit, 0 miss, -1 the reference throws.
@@ -1551,10 +1597,8 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
             const RayBox rb = make_raybox(w.o, w.d);
             const size_t id = (size_t)q * K + j;
             auto emit = [&](int node) {
-                const RtNode &nd = S.node[node];
-                if (nd.n_ent == 0) return;
-                if (L.cull && rb.ok && !ray_box(nd.box, rb)) return;
-                if (n < L.cand_cap) L.cand[(size_t)n * stride + id] = node;
+                if (!node_candidate(S, node, L.cull != 0, rb)) return;
+                if (n < L.cand_cap) cand_store(L.cand, n, (uint32_t)stride, (uint32_t)id, node);
                 n++;
             };
             const int r = walker_run<true>(S, w, emit, stop);
@@ -1602,7 +1646,7 @@ __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
             const RayBox rb = make_raybox(o, d);
             const int n = cn >> 3;
             for (int k = 0; k < n; k++) {
-                const int node = L.cand[(size_t)k * stride + id];
+                const int node = cand_load(L.cand, k, (uint32_t)stride, (uint32_t)id);
                 const RtNode &nd = S.node[node];
                 const int4 ent = make_int4(nd.ent_begin, nd.n_ent, nd.bvh_root, 0);
                 Hit h;
@@ -1683,10 +1727,8 @@ __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
             continue;
         }
         auto emit = [&](int node) {
-            const RtNode &nd = S.node[node];
-            if (nd.n_ent == 0) return;
-            if (L.cull && rb.ok && !ray_box(nd.box, rb)) return;
-            if (n < L.cand_cap) L.cand[(size_t)n * stride + q] = node;
+            if (!node_candidate(S, node, L.cull != 0, rb)) return;
+            if (n < L.cand_cap) cand_store(L.cand, n, (uint32_t)stride, (uint32_t)q, node);
             n++;
         };
         walker_trip<false, false>(S, w, emit, -1, res);
@@ -1725,10 +1767,8 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
             end = src.rec ? 3 : 1;
         } else {
             auto emit = [&](int node) {
-                const RtNode &nd = S.node[node];               // one cache line: count + root box + cube
-                if (nd.n_ent == 0) return;
-                if (L.cull && rb.ok && !ray_box(nd.box, rb)) return;
-                if (n < L.cand_cap) L.cand[(size_t)n * stride + src.id] = node;
+                if (!node_candidate(S, node, L.cull != 0, rb)) return;
+                if (n < L.cand_cap) cand_store(L.cand, n, (uint32_t)stride, (uint32_t)src.id, node);
                 n++;
             };
             const int r = walker_run<false, true>(S, w, emit);
@@ -1812,7 +1852,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
             const RayBox rb = make_raybox(src.o, src.d);
             const int n = cn >> 2;
             for (int k = 0; k < n; k++) {
-                const int node = L.cand[(size_t)k * stride + src.id];
+                const int node = cand_load(L.cand, k, (uint32_t)stride, (uint32_t)src.id);
                 const RtNode &nd = S.node[node];               // the line k_walk read for this candidate
                 const int4 ent = make_int4(nd.ent_begin, nd.n_ent, nd.bvh_root, 0);
                 Hit h;
