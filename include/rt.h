@@ -48,6 +48,8 @@ extern "C" {
 #define RT_E_NODEVICE    -6   /* no HIP device                                                */
 #define RT_E_TREE        -7   /* octree growth error (reference TreeOutsideGrowError /
                                  "Node index out of range"), builder only                      */
+#define RT_E_STALE       -8   /* rt_apply_edit: the resident scene cannot take the edit; upload
+                                 the scene in full                                              */
 
 /* ---- scene ----------------------------------------------------------------------------- */
 /* Entity kinds.  SPHERE = SphereEntity (src/entities/entity_sphere.ts:29-102), BOX = BoxEntity
@@ -311,6 +313,20 @@ int  rt_debug_walk(rt_ctx *ctx, const double origin[3], const double dir[3], int
  * produced them for `cam` (Camera.get_dir_for_each_pixel, src/view/camera.ts:207-250). */
 int  rt_debug_camera_dirs(rt_ctx *ctx, const rt_camera_desc *cam, double *dirs_out);
 
+/* Debug (no GPU): the RCCL call sequence of `frames` multi-device frames.  n_ctx
+ * contexts (frames in flight) over devices 0..n_dev-1 each take communicators from ncclCommInitAll
+ * of the library rt_rccl() loads (RT_RCCL_LIB: a recording stub); frame f runs on context
+ * f % n_ctx and issues exactly frame_multi's collectives (the shared rt_rccl_frame: a blend's
+ * scatter group, the devices' traces, the gather group) over placeholder stream and buffer handles:
+ * stream of (ctx, device) = (ctx + 1) << 24 | (device + 1) << 8; device part buffer of array a =
+ * (ctx + 1) << 40 | (device + 1) << 32 | (a + 1) << 24; stacked buffer = (ctx + 1) << 40 | 0xff << 32.
+ * on_trace(ctx, device) is called where frame_multi launches a device's kernels.  The communicators
+ * are destroyed at the end.  Makes no HIP call.  (Multi-GPU is this build's addition, SURVEY §8(e);
+ * it replaces no reference interface.) */
+typedef void (*rt_trace_hook)(int32_t ctx, int32_t device);
+int  rt_debug_rccl_frames(int32_t n_dev, int32_t n_ctx, int32_t frames, int32_t width, int32_t height,
+                          int32_t stripe, int32_t blend, int32_t ids, rt_trace_hook on_trace);
+
 /* ---- device-resident exposure buffer: statistics and tone mapping ---- */
 typedef struct rt_exposure_stats {
     double mean;       /* ExposureBuffer.get_mean()              src/view/exposure_buffer.ts:90-104  */
@@ -380,6 +396,59 @@ int  rt_builder_desc(rt_builder *b, const rt_shade *shades, int32_t n_shades,
  * ctx's devices first: no frame may be in flight. */
 int  rt_builder_sync(rt_ctx *ctx, rt_builder *b, const rt_shade *shades, int32_t n_shades,
                      const double *substance_ri, int32_t n_substances, rt_update_stats *stats);
+
+/* ---- O(edit) scene updates from a host that journals its own edits (the JS drop-in) ---- */
+/* The edit of the resident scene since the last rt_upload_scene / rt_update_scene(full) /
+ * rt_apply_edit on ctx, in the resident scene's node slots: a full upload numbers the slots in DFS
+ * order (slot k = DFS id k of that upload) and every later node takes the next slot.  The host names
+ * what changed (the same content rt_builder_sync derives from the native builder's journal):
+ *   rec_*:  node records to (re)write, ascending slots: every new node, and existing nodes that
+ *           gained a child (cube pos.xyz + size, 8 child slots with -1 empty, parent slot with -1
+ *           for the root, index_within_parent as src/octree_space.ts:113-125 computes it);
+ *   set_*:  every node whose EntitySet or a member entity changed, and every new node: its whole
+ *           Set in insertion order (entity id, RT_ENT_* type, shade row, 9 geometry doubles in
+ *           rt_scene_desc.ent_geom's layout);
+ *   sub_*:  entities whose substance is (re)sent;
+ *   dfs_*:  when nodes were created, the new slots' DFS ids and the shift of the existing ones
+ *           (old id a -> a + #{j : dfs_shift[j] <= a}, ascending);
+ * plus the whole shade and substance tables (image rows must name images already resident).
+ * Replaces the same reference edits as rt_update_scene (add_entity_to_octree, Entity.set_octree /
+ * _set_pos / set_material / set_texture / set_substance: src/octree_entity.ts:174-188,
+ * src/entity.ts:50-56) in O(edit) on the host, without a linearisation or a diff of the scene.
+ * Returns RT_OK, or RT_E_STALE when the store cannot take the edit (never uploaded, or its pools
+ * are mostly garbage): the resident scene is left as it was and the host uploads the scene through
+ * rt_update_scene (which compacts) or rt_upload_scene.
+ * Synchronises ctx's devices first: no frame may be in flight. */
+typedef struct rt_edit_desc {
+    int32_t n_slots, n_entities;     /* node slots and entities after the edit                    */
+    int32_t n_rec;
+    const int32_t *rec_slot;         /* [n_rec]                                                  */
+    const double *rec_cube;          /* [n_rec * 4]                                              */
+    const int32_t *rec_child;        /* [n_rec * 8]                                              */
+    const int32_t *rec_up;           /* [n_rec * 2]                                              */
+    int32_t n_set;
+    const int32_t *set_slot, *set_begin, *set_count;   /* [n_set]; members set_begin .. +count  */
+    int32_t n_member;
+    const int32_t *set_ent, *set_type, *set_shade;     /* [n_member]                            */
+    const double *set_geom;                            /* [n_member * 9]                        */
+    int32_t n_sub;
+    const int32_t *sub_ent, *sub_val;                  /* [n_sub] entity id, substance (-1 none) */
+    int32_t n_dfs_new, n_dfs_shift;
+    const int32_t *dfs_new_slot, *dfs_new_val;         /* [n_dfs_new]                           */
+    const int32_t *dfs_shift;                          /* [n_dfs_shift]                         */
+    int32_t scatter;                                   /* a listed entity has a rough mirror    */
+    int32_t n_shades, n_substances;
+    const rt_shade *shades;
+    const double *substance_ri;
+} rt_edit_desc;
+int  rt_apply_edit(rt_ctx *ctx, const rt_edit_desc *edit, rt_update_stats *stats);
+
+/* The resident node slot of each DFS id (out[k] = slot of the scene desc's node k) after the last
+ * rt_upload_scene / rt_update_scene, for a host that journals edits in slots (rt_apply_edit): a full
+ * upload numbers slots in DFS order, an incremental rt_update_scene keeps old nodes in their slots.
+ * n = the desc's node count.  RT_E_STALE after an rt_apply_edit / rt_builder_sync edit (the map is
+ * the host's own then).  Replaces no reference interface. */
+int  rt_scene_node_slots(rt_ctx *ctx, int32_t *out, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -84,7 +84,14 @@ struct RtDevice {
     std::vector<std::array<hipEvent_t, 2>> ev;   // trace-kernel timing ring
     int ev_next = 0, ev_count = 0;
     hipEvent_t sync = nullptr;                   // cross-stream / cross-device ordering
-    int32_t *h_ctr = nullptr;                    // pinned: the work counters of a recent frame (grid hints)
+    // grid hints (rt_kernels.hip level_blocks): each frame copies its work counters back into one of
+    // two pinned buffers (ctr_w) and records ctr_ev; the host reads only a copy whose event is done,
+    // into ctr_snap, so launches never read a buffer a transfer may still be writing
+    int32_t *h_ctr = nullptr;                    // pinned: 2 x RT_CTR_INTS
+    hipEvent_t ctr_ev[2] = {};
+    bool ctr_pend[2] = {};
+    uint64_t ctr_seq[2] = {}, ctr_snap_seq = 0, ctr_frames = 0;
+    std::vector<int32_t> ctr_snap;               // the newest completed copy (-1: none yet)
 };
 
 }  // namespace
@@ -144,6 +151,10 @@ static void release_device(RtDevice &d)
     d.ev.clear();
     if (d.sync) (void)hipEventDestroy(d.sync);
     if (d.h_ctr) (void)hipHostFree(d.h_ctr);
+    for (hipEvent_t &e : d.ctr_ev) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
     if (d.stream) (void)hipStreamDestroy(d.stream);
     d.sync = nullptr;
     d.h_ctr = nullptr;
@@ -154,13 +165,6 @@ static int use_device(const RtDevice &d)
 {
     HIP_TRY(hipSetDevice(d.device));
     return RT_OK;
-}
-
-static int rccl_try(int rc, const char *what)
-{
-    if (rc == 0) return RT_OK;
-    const RtRccl *R = rt_rccl();
-    return rt_set_error(RT_E_HIP, "%s: RCCL error %d (%s)", what, rc, R ? R->error_string(rc) : "?");
 }
 
 static int pow2_at_most_64(int v)
@@ -262,7 +266,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (r == RT_OK && c->gather == RT_GATHER_RCCL) {
         const RtRccl *R = rt_rccl();
         if (!R) r = rt_set_error(RT_E_HIP, "rt_create: %s (RT_CREATE_PEER_GATHER gathers without RCCL)", rt_rccl_error());
-        else r = rccl_try(R->comm_init_all(c->comm, nd, devs), "ncclCommInitAll");
+        else r = rt_rccl_try(R->comm_init_all(c->comm, nd, devs), "ncclCommInitAll");
     }
     if (r == RT_OK && !(c->store = rt_store_new(c->bvh_sah, nd, devs, streams)))
         r = rt_set_error(RT_E_INVALID, "rt_create: out of memory");
@@ -375,6 +379,92 @@ extern "C" int rt_builder_sync(rt_ctx *c, rt_builder *b, const rt_shade *shades,
     return RT_OK;
 }
 
+extern "C" int rt_apply_edit(rt_ctx *c, const rt_edit_desc *d, rt_update_stats *stats)
+{
+    if (!c || !d) return rt_set_error(RT_E_INVALID, "rt_apply_edit: null argument");
+    if (!c->has_scene) return rt_set_error(RT_E_STALE, "rt_apply_edit: no resident scene");
+    const RtDevScene &S0 = c->dev[0].scene;
+    auto bad = [](const char *what, long long v) { return rt_set_error(RT_E_INVALID, "rt_apply_edit: %s (%lld)", what, v); };
+    if (d->n_slots < S0.n_nodes || d->n_entities < 0 || d->n_rec < 0 || d->n_set < 0 || d->n_member < 0 ||
+        d->n_sub < 0 || d->n_dfs_new < 0 || d->n_dfs_shift < 0 || d->n_shades < 0 || d->n_substances < 0)
+        return bad("bad counts; n_slots", d->n_slots);
+    if ((d->n_rec && (!d->rec_slot || !d->rec_cube || !d->rec_child || !d->rec_up)) ||
+        (d->n_set && (!d->set_slot || !d->set_begin || !d->set_count)) ||
+        (d->n_member && (!d->set_ent || !d->set_type || !d->set_shade || !d->set_geom)) ||
+        (d->n_sub && (!d->sub_ent || !d->sub_val)) || (d->n_dfs_new && (!d->dfs_new_slot || !d->dfs_new_val)) ||
+        (d->n_dfs_shift && !d->dfs_shift) || (d->n_shades && !d->shades) || (d->n_substances && !d->substance_ri))
+        return bad("null array", 0);
+    for (int i = 0; i < d->n_shades; i++)
+        if (d->shades[i].image < 0 || d->shades[i].image > S0.n_images) return bad("shade image not resident", i);
+    RtEdit e;
+    e.n_slots = d->n_slots;
+    e.n_entities = d->n_entities;
+    e.scatter = d->scatter != 0;
+    for (int k = 0; k < d->n_rec; k++) {
+        const int sl = d->rec_slot[k];
+        if (sl < 0 || sl >= d->n_slots || (k && sl <= d->rec_slot[k - 1])) return bad("rec_slot", sl);
+        for (int j = 0; j < 8; j++)
+            if (d->rec_child[8 * k + j] < -1 || d->rec_child[8 * k + j] >= d->n_slots) return bad("rec_child", sl);
+        if (d->rec_up[2 * k] < -1 || d->rec_up[2 * k] >= d->n_slots) return bad("rec_up", sl);
+    }
+    e.rec_slot.assign(d->rec_slot, d->rec_slot + d->n_rec);
+    e.rec_cube.assign(d->rec_cube, d->rec_cube + 4 * (size_t)d->n_rec);
+    e.rec_child.assign(d->rec_child, d->rec_child + 8 * (size_t)d->n_rec);
+    e.rec_up.assign(d->rec_up, d->rec_up + 2 * (size_t)d->n_rec);
+    for (int k = 0; k < d->n_set; k++) {
+        const int sl = d->set_slot[k], b = d->set_begin[k], n = d->set_count[k];
+        if (sl < 0 || sl >= d->n_slots) return bad("set_slot", sl);
+        if (b < 0 || n < 0 || (long long)b + n > d->n_member) return bad("set_begin / set_count", k);
+    }
+    for (int i = 0; i < d->n_member; i++) {
+        if (d->set_ent[i] < 0 || d->set_ent[i] >= d->n_entities) return bad("set_ent", d->set_ent[i]);
+        if (d->set_type[i] < RT_ENT_SPHERE || d->set_type[i] > RT_ENT_FACE) return bad("set_type", d->set_type[i]);
+        if (d->set_shade[i] < 0 || d->set_shade[i] >= d->n_shades) return bad("set_shade", d->set_shade[i]);
+    }
+    e.set_slot.assign(d->set_slot, d->set_slot + d->n_set);
+    e.set_begin.assign(d->set_begin, d->set_begin + d->n_set);
+    e.set_count.assign(d->set_count, d->set_count + d->n_set);
+    e.set_ent.assign(d->set_ent, d->set_ent + d->n_member);
+    e.set_type.assign(d->set_type, d->set_type + d->n_member);
+    e.set_shade.assign(d->set_shade, d->set_shade + d->n_member);
+    e.set_geom.assign(d->set_geom, d->set_geom + 9 * (size_t)d->n_member);
+    for (int i = 0; i < d->n_sub; i++)
+        if (d->sub_ent[i] < 0 || d->sub_ent[i] >= d->n_entities || (i && d->sub_ent[i] <= d->sub_ent[i - 1]))
+            return bad("sub_ent (ascending, unique)", d->sub_ent[i]);
+    e.sub_ent.assign(d->sub_ent, d->sub_ent + d->n_sub);
+    e.sub_val.assign(d->sub_val, d->sub_val + d->n_sub);
+    for (int i = 0; i < d->n_dfs_new; i++)
+        if (d->dfs_new_slot[i] < S0.n_nodes || d->dfs_new_slot[i] >= d->n_slots) return bad("dfs_new_slot", d->dfs_new_slot[i]);
+    for (int i = 1; i < d->n_dfs_shift; i++)
+        if (d->dfs_shift[i] < d->dfs_shift[i - 1]) return bad("dfs_shift (ascending)", i);
+    e.dfs_new_slot.assign(d->dfs_new_slot, d->dfs_new_slot + d->n_dfs_new);
+    e.dfs_new_val.assign(d->dfs_new_val, d->dfs_new_val + d->n_dfs_new);
+    e.dfs_shift.assign(d->dfs_shift, d->dfs_shift + d->n_dfs_shift);
+    DevGuard guard;
+    RtDevScene scenes[RT_MAX_DEVICES];
+    c->has_scene = false;
+    const int r = rt_store_apply_edit(c->store, e, d->shades, d->n_shades, d->substance_ri, d->n_substances, scenes, stats);
+    if (r < 0) return r;
+    if (r != RT_OK) {                         // refused before any change: the resident scene stands
+        c->has_scene = true;
+        return rt_set_error(RT_E_STALE, "rt_apply_edit: the resident scene needs a full upload");
+    }
+    for (int k = 0; k < c->n_dev; k++) c->dev[k].scene = scenes[k];
+    c->scatter = e.scatter;
+    c->has_scene = true;
+    return RT_OK;
+}
+
+extern "C" int rt_scene_node_slots(rt_ctx *c, int32_t *out, int32_t n)
+{
+    if (!c || !out || n < 0) return rt_set_error(RT_E_INVALID, "rt_scene_node_slots: bad argument");
+    if (!c->has_scene) return rt_set_error(RT_E_NOSCENE, "rt_scene_node_slots: no scene uploaded");
+    const int r = rt_store_node_slots(c->store, out, n);
+    if (r < 0) return rt_set_error(RT_E_INVALID, "rt_scene_node_slots: n = %d is not the node count", n);
+    if (r > 0) return rt_set_error(RT_E_STALE, "rt_scene_node_slots: the resident scene was edited since its desc");
+    return RT_OK;
+}
+
 static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg)
 {
     if (!c || !cam || !cfg) return rt_set_error(RT_E_INVALID, "null argument");
@@ -432,10 +522,31 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.fault = (int32_t *)d.b_fault.p;
     L.cull = (c->flags & RT_CREATE_NO_CULL) ? 0 : 1;
     L.ctr = (int32_t *)d.b_ctr.p;
-    if (!d.h_ctr && hipHostMalloc((void **)&d.h_ctr, sizeof(int32_t) * RT_CTR_INTS, hipHostMallocDefault) == hipSuccess)
-        for (int i = 0; i < RT_CTR_INTS; i++) d.h_ctr[i] = -1;        // unknown until a frame completes
-    (void)hipGetLastError();
-    L.ctr_hint = c->hints ? d.h_ctr : nullptr;
+    if (c->hints) {
+        if (!d.h_ctr) {
+            if (hipHostMalloc((void **)&d.h_ctr, 2 * sizeof(int32_t) * RT_CTR_INTS, hipHostMallocDefault) != hipSuccess ||
+                hipEventCreateWithFlags(&d.ctr_ev[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&d.ctr_ev[1], hipEventDisableTiming) != hipSuccess)
+                return rt_set_error(RT_E_HIP, "prepare: grid-hint buffers");
+            d.ctr_snap.assign(RT_CTR_INTS, -1);                             // unknown until a frame completes
+        }
+        for (int i = 0; i < 2; i++)
+            if (d.ctr_pend[i] && hipEventQuery(d.ctr_ev[i]) == hipSuccess) {
+                d.ctr_pend[i] = false;
+                if (d.ctr_seq[i] > d.ctr_snap_seq) {
+                    memcpy(d.ctr_snap.data(), d.h_ctr + (size_t)i * RT_CTR_INTS, sizeof(int32_t) * RT_CTR_INTS);
+                    d.ctr_snap_seq = d.ctr_seq[i];
+                }
+            }
+        (void)hipGetLastError();                                            // hipErrorNotReady
+        // this frame's copy goes to a buffer without a transfer in flight, else to the older one
+        const int w = !d.ctr_pend[0] ? 0 : (!d.ctr_pend[1] ? 1 : (d.ctr_seq[0] < d.ctr_seq[1] ? 0 : 1));
+        d.ctr_pend[w] = true;
+        d.ctr_seq[w] = ++d.ctr_frames;
+        L.ctr_hint = d.ctr_snap.data();
+        L.ctr_out = d.h_ctr + (size_t)w * RT_CTR_INTS;
+        L.ctr_done = d.ctr_ev[w];
+    }
     L.occ = c->occ;
     L.diag = c->diag;
     L.cont_group = c->cont_group;
@@ -546,10 +657,7 @@ static int frame_multi(rt_ctx *c, const rt_camera_desc *cam, const rt_config_des
     const size_t st_rgb = (size_t)N * PS * 12, st_ids = ids ? (size_t)N * PS * 9 : 0;
     if ((r = c->g_stack.ensure(st_rgb + st_ids + 16)) != RT_OK) return r;
     uint8_t *stack = (uint8_t *)c->g_stack.p;
-    float *stack_rgb = (float *)stack;
-    int32_t *stack_he = (int32_t *)(stack + st_rgb);
-    int32_t *stack_hn = stack_he + (size_t)N * PS;
-    uint8_t *stack_st = (uint8_t *)(stack_hn + (size_t)N * PS);
+    float *stack_rgb = (float *)stack;       // the rgb parts (rt_gather_arrays' layout)
     if (caller && caller != d0.stream) {
         HIP_TRY(hipEventRecord(d0.sync, caller));
         HIP_TRY(hipStreamWaitEvent(d0.stream, d0.sync, 0));
@@ -579,68 +687,49 @@ static int frame_multi(rt_ctx *c, const rt_camera_desc *cam, const rt_config_des
     }
     const RtRccl *R = c->gather == RT_GATHER_RCCL ? rt_rccl() : nullptr;
     if (c->gather == RT_GATHER_RCCL && !R) return rt_set_error(RT_E_HIP, "RCCL unavailable: %s", rt_rccl_error());
-    if (blend) {
+    void *part_rgb[RT_MAX_DEVICES], *part_he[RT_MAX_DEVICES], *part_hn[RT_MAX_DEVICES], *part_st[RT_MAX_DEVICES];
+    void *streams[RT_MAX_DEVICES];
+    for (int k = 0; k < N; k++) {
+        part_rgb[k] = c->dev[k].b_rgb.p;
+        part_he[k] = c->dev[k].b_hit_e.p;
+        part_hn[k] = c->dev[k].b_hit_n.p;
+        part_st[k] = c->dev[k].b_status.p;
+        streams[k] = c->dev[k].stream;
+    }
+    RtGatherArr arrs[4];
+    const int n_arr = rt_gather_arrays(arrs, N, PS, ids, stack, part_rgb, part_he, part_hn, part_st);
+    auto trace = [&](int k) -> int {
+        RtDevice &d = c->dev[k];
+        int rr;
+        if ((rr = use_device(d)) != RT_OK) return rr;
+        hipEvent_t *ev = next_events(d);
+        return rt_launch_frame(L[k], d.stream, ev[0], ev[1]);
+    };
+    if (blend) {   // dev[0] deals the current frame out into the stacked parts
         HIP_TRY(hipSetDevice(d0.device));
         if ((r = rt_launch_stripes(o.rgb, stack_rgb, H, N, stripe, max_rows, (size_t)W * 12, 0, d0.stream)) != RT_OK)
             return r;
-        if (R) {
-            if ((r = rccl_try(R->group_start(), "ncclGroupStart")) != RT_OK) return r;
-            for (int k = 0; k < N; k++)
-                if ((r = rccl_try(R->scatter(stack_rgb, c->dev[k].b_rgb.p, PS * 3, RT_NCCL_FLOAT32, 0, c->comm[k],
-                                             c->dev[k].stream), "ncclScatter")) != RT_OK) {
-                    (void)R->group_end();
-                    return r;
-                }
-            if ((r = rccl_try(R->group_end(), "ncclGroupEnd")) != RT_OK) return r;
-        } else {
+    }
+    if (R) {
+        if ((r = rt_rccl_frame(R, N, c->comm, streams, blend ? &arrs[0] : nullptr, arrs, n_arr, trace)) != RT_OK)
+            return r;
+    } else {
+        if (blend) {
             for (int k = 0; k < N; k++)
                 HIP_TRY(hipMemcpyPeerAsync(c->dev[k].b_rgb.p, c->dev[k].device, stack_rgb + (size_t)k * PS * 3,
                                            d0.device, sizeof(float) * 3 * PS, d0.stream));
             for (int k = 1; k < N; k++)
                 if ((r = order_after(d0, c->dev[k].stream)) != RT_OK) return r;
         }
-    }
-    for (int k = 0; k < N; k++) {
-        RtDevice &d = c->dev[k];
-        if ((r = use_device(d)) != RT_OK) return r;
-        hipEvent_t *ev = next_events(d);
-        if ((r = rt_launch_frame(L[k], d.stream, ev[0], ev[1])) != RT_OK) return r;
-    }
-    struct Arr { void *dev_buf[RT_MAX_DEVICES]; void *stack; size_t count, elem; int dtype; };
-    Arr arrs[4];
-    int n_arr = 0;
-    arrs[n_arr] = {{}, stack_rgb, PS * 3, 4, RT_NCCL_FLOAT32};
-    for (int k = 0; k < N; k++) arrs[n_arr].dev_buf[k] = c->dev[k].b_rgb.p;
-    n_arr++;
-    if (ids) {
-        arrs[n_arr] = {{}, stack_he, PS, 4, RT_NCCL_INT32};
-        for (int k = 0; k < N; k++) arrs[n_arr].dev_buf[k] = c->dev[k].b_hit_e.p;
-        n_arr++;
-        arrs[n_arr] = {{}, stack_hn, PS, 4, RT_NCCL_INT32};
-        for (int k = 0; k < N; k++) arrs[n_arr].dev_buf[k] = c->dev[k].b_hit_n.p;
-        n_arr++;
-        arrs[n_arr] = {{}, stack_st, PS, 1, RT_NCCL_UINT8};
-        for (int k = 0; k < N; k++) arrs[n_arr].dev_buf[k] = c->dev[k].b_status.p;
-        n_arr++;
-    }
-    if (R) {
-        if ((r = rccl_try(R->group_start(), "ncclGroupStart")) != RT_OK) return r;
-        for (int a = 0; a < n_arr; a++)
-            for (int k = 0; k < N; k++)
-                if ((r = rccl_try(R->gather(arrs[a].dev_buf[k], arrs[a].stack, arrs[a].count, arrs[a].dtype, 0,
-                                            c->comm[k], c->dev[k].stream), "ncclGather")) != RT_OK) {
-                    (void)R->group_end();
-                    return r;
-                }
-        if ((r = rccl_try(R->group_end(), "ncclGroupEnd")) != RT_OK) return r;
-    } else {
+        for (int k = 0; k < N; k++)
+            if ((r = trace(k)) != RT_OK) return r;
         for (int k = 1; k < N; k++)
             if ((r = order_after(c->dev[k], d0.stream)) != RT_OK) return r;
         HIP_TRY(hipSetDevice(d0.device));
         for (int a = 0; a < n_arr; a++)
             for (int k = 0; k < N; k++)
                 HIP_TRY(hipMemcpyPeerAsync((uint8_t *)arrs[a].stack + (size_t)k * arrs[a].count * arrs[a].elem,
-                                           d0.device, arrs[a].dev_buf[k], c->dev[k].device,
+                                           d0.device, arrs[a].part[k], c->dev[k].device,
                                            arrs[a].count * arrs[a].elem, d0.stream));
         // a device's next frame rewrites its part buffers only after dev[0] has copied them
         for (int k = 1; k < N; k++)
@@ -649,11 +738,11 @@ static int frame_multi(rt_ctx *c, const rt_camera_desc *cam, const rt_config_des
     HIP_TRY(hipSetDevice(d0.device));
     if ((r = rt_launch_stripes(stack_rgb, o.rgb, H, N, stripe, max_rows, (size_t)W * 12, 1, d0.stream)) != RT_OK)
         return r;
-    if (o.hit_e && (r = rt_launch_stripes(stack_he, o.hit_e, H, N, stripe, max_rows, (size_t)W * 4, 1, d0.stream)))
+    if (o.hit_e && (r = rt_launch_stripes(arrs[1].stack, o.hit_e, H, N, stripe, max_rows, (size_t)W * 4, 1, d0.stream)))
         return r;
-    if (o.hit_n && (r = rt_launch_stripes(stack_hn, o.hit_n, H, N, stripe, max_rows, (size_t)W * 4, 1, d0.stream)))
+    if (o.hit_n && (r = rt_launch_stripes(arrs[2].stack, o.hit_n, H, N, stripe, max_rows, (size_t)W * 4, 1, d0.stream)))
         return r;
-    if (o.status && (r = rt_launch_stripes(stack_st, o.status, H, N, stripe, max_rows, (size_t)W, 1, d0.stream)))
+    if (o.status && (r = rt_launch_stripes(arrs[3].stack, o.status, H, N, stripe, max_rows, (size_t)W, 1, d0.stream)))
         return r;
     if (caller && caller != d0.stream) {
         HIP_TRY(hipEventRecord(d0.sync, d0.stream));
@@ -1099,6 +1188,48 @@ extern "C" int rt_debug_walk(rt_ctx *c, const double origin[3], const double dir
     HIP_TRY(hipMemcpy(out_octant, d_oct, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
     *n_out = n;
     return RT_OK;
+}
+
+extern "C" int rt_debug_rccl_frames(int32_t n_dev, int32_t n_ctx, int32_t frames, int32_t width, int32_t height,
+                                    int32_t stripe, int32_t blend, int32_t ids, rt_trace_hook on_trace)
+{
+    if (n_dev < 1 || n_dev > RT_MAX_DEVICES || n_ctx < 1 || n_ctx > 64 || frames < 0 || width < 1 || height < 1 ||
+        stripe < 1)
+        return rt_set_error(RT_E_INVALID, "rt_debug_rccl_frames: bad arguments");
+    const RtRccl *R = rt_rccl();
+    if (!R) return rt_set_error(RT_E_HIP, "rt_debug_rccl_frames: %s", rt_rccl_error());
+    std::vector<std::array<void *, RT_MAX_DEVICES>> comms(n_ctx);
+    int devs[RT_MAX_DEVICES];
+    for (int k = 0; k < n_dev; k++) devs[k] = k;
+    int r = RT_OK;
+    int made = 0;
+    for (; made < n_ctx && r == RT_OK; made++)
+        r = rt_rccl_try(R->comm_init_all(comms[made].data(), n_dev, devs), "ncclCommInitAll");
+    // frame_multi's part size: the most rows any part owns, times the width
+    int max_rows = 0;
+    for (int p = 0; p < n_dev; p++) max_rows = std::max(max_rows, rt_part_rows(height, p, n_dev, stripe));
+    const size_t PS = (size_t)max_rows * (size_t)width;
+    for (int f = 0; f < frames && r == RT_OK; f++) {
+        const int x = f % n_ctx;
+        const uint64_t cx = (uint64_t)(x + 1);
+        void *streams[RT_MAX_DEVICES], *part[4][RT_MAX_DEVICES];
+        for (int k = 0; k < n_dev; k++) {
+            streams[k] = (void *)(uintptr_t)(cx << 24 | (uint64_t)(k + 1) << 8);
+            for (int a = 0; a < 4; a++) part[a][k] = (void *)(uintptr_t)(cx << 40 | (uint64_t)(k + 1) << 32 | (uint64_t)(a + 1) << 24);
+        }
+        RtGatherArr arrs[4];
+        const int n_arr = rt_gather_arrays(arrs, n_dev, PS, ids != 0, (void *)(uintptr_t)(cx << 40 | 0xffull << 32),
+                                           part[0], part[1], part[2], part[3]);
+        auto trace = [&](int k) -> int {
+            if (on_trace) on_trace(x, k);
+            return RT_OK;
+        };
+        r = rt_rccl_frame(R, n_dev, comms[x].data(), streams, blend ? &arrs[0] : nullptr, arrs, n_arr, trace);
+    }
+    for (int i = 0; i < made; i++)
+        for (int k = 0; k < n_dev; k++)
+            if (comms[i][k]) (void)R->comm_destroy(comms[i][k]);
+    return r;
 }
 
 extern "C" int rt_debug_camera_dirs(rt_ctx *c, const rt_camera_desc *cam, double *dirs_out)

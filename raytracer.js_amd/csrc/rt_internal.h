@@ -124,6 +124,9 @@ int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, 
 // Every upload / update / edit of a store bumps its epoch: a builder's journal is only valid
 // against the store state it was synced with.
 uint64_t rt_store_epoch(const RtSceneStore *st);
+// The slot of each DFS id of the last uploaded desc (0; 1 when the mirrors are not kept, i.e. after
+// an edit; -1 when n is not the node count).
+int rt_store_node_slots(const RtSceneStore *st, int32_t *out, int32_t n);
 
 // An edit of the resident scene made through the native builder since its last rt_builder_sync
 // (rt_builder.cpp builds it from the builder's journal, rt_scene.hip applies it): O(edit) on the
@@ -195,7 +198,9 @@ struct RtLaunch {
     int32_t refill;                             // wide bounce levels: idle lanes that take new rays (0: off; RT_REFILL)
     int32_t refill_always;                      // refill every wide level, not only where a recent frame had one (tests)
     int32_t seg_max;                            // bounce levels of more rays run unsegmented (0: no limit; RT_SEG_MAX)
-    int32_t *ctr_hint;                          // pinned host copy of a recent frame's ctr (-1: none yet), or null
+    const int32_t *ctr_hint;                    // host snapshot of a recent frame's ctr (-1: none yet), or null
+    int32_t *ctr_out;                           // pinned: this frame's ctr is copied here at its end (or null)
+    void *ctr_done;                             // hipEvent_t recorded after that copy
 };
 
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };
@@ -231,8 +236,77 @@ struct RtRccl {
     int (*group_end)(void);
     const char *(*error_string)(int);
 };
-const RtRccl *rt_rccl(void);        // null when librccl is unavailable (rt_rccl_error() says why)
+const RtRccl *rt_rccl(void);        // null when librccl is unavailable (rt_rccl_error() says why);
+                                    // RT_RCCL_LIB names another library (the CPU check's recording stub)
 const char *rt_rccl_error(void);
+int rt_rccl_try(int rc, const char *what);   // RT_OK, or RT_E_HIP with RCCL's message
+
+// One array of a multi-device frame as the collectives move it: each device's part buffer (count
+// elements) and its place in device 0's stacked buffer (device k's part at stack + k * count * elem).
+struct RtGatherArr {
+    void *part[RT_MAX_DEVICES];
+    void *stack;
+    size_t count, elem;
+    int dtype;
+};
+
+// The output arrays of a multi-device frame over the stacked buffer at `stack` (N parts of PS
+// pixels: rgb f32 x3 | hit entity i32 | hit node i32 | status u8) and the devices' part buffers
+// (ids: the id arrays are gathered too).  Returns the number of arrays (1 or 4).
+static inline int rt_gather_arrays(RtGatherArr *out, int N, size_t PS, bool ids, void *stack, void *const *rgb,
+                                   void *const *hit_e, void *const *hit_n, void *const *status)
+{
+    uint8_t *s = (uint8_t *)stack;
+    const size_t st_rgb = (size_t)N * PS * 12;
+    out[0] = RtGatherArr{{}, s, PS * 3, 4, RT_NCCL_FLOAT32};
+    for (int k = 0; k < N; k++) out[0].part[k] = rgb[k];
+    if (!ids) return 1;
+    out[1] = RtGatherArr{{}, s + st_rgb, PS, 4, RT_NCCL_INT32};
+    out[2] = RtGatherArr{{}, s + st_rgb + (size_t)N * PS * 4, PS, 4, RT_NCCL_INT32};
+    out[3] = RtGatherArr{{}, s + st_rgb + (size_t)N * PS * 8, PS, 1, RT_NCCL_UINT8};
+    for (int k = 0; k < N; k++) {
+        out[1].part[k] = hit_e[k];
+        out[2].part[k] = hit_n[k];
+        out[3].part[k] = status[k];
+    }
+    return 4;
+}
+
+// The RCCL calls of one multi-device frame, issued from one thread over the context's
+// communicators (comm[k] and stream[k] of device k):
+//   1. a blend (`deal` non-null): device 0's dealt frame scattered to every part, one group;
+//   2. trace(k) for every device (its kernels on stream[k]);
+//   3. every output array gathered to device 0's stack, one group (array-major, devices in order).
+// frame_multi (rt_api.hip) and the CPU check of the call sequence (rt_debug_rccl_frames, against a
+// recording stub library) both run this function.
+template <typename Trace>
+int rt_rccl_frame(const RtRccl *R, int N, void *const *comm, void *const *stream, const RtGatherArr *deal,
+                  const RtGatherArr *arrs, int n_arr, Trace &&trace)
+{
+    int r;
+    if (deal) {
+        if ((r = rt_rccl_try(R->group_start(), "ncclGroupStart")) != RT_OK) return r;
+        for (int k = 0; k < N; k++)
+            if ((r = rt_rccl_try(R->scatter(deal->stack, deal->part[k], deal->count, deal->dtype, 0, comm[k], stream[k]),
+                                 "ncclScatter")) != RT_OK) {
+                (void)R->group_end();
+                return r;
+            }
+        if ((r = rt_rccl_try(R->group_end(), "ncclGroupEnd")) != RT_OK) return r;
+    }
+    for (int k = 0; k < N; k++)
+        if ((r = trace(k)) != RT_OK) return r;
+    if ((r = rt_rccl_try(R->group_start(), "ncclGroupStart")) != RT_OK) return r;
+    for (int a = 0; a < n_arr; a++)
+        for (int k = 0; k < N; k++)
+            if ((r = rt_rccl_try(R->gather(arrs[a].part[k], arrs[a].stack, arrs[a].count, arrs[a].dtype, 0, comm[k],
+                                           stream[k]),
+                                 "ncclGather")) != RT_OK) {
+                (void)R->group_end();
+                return r;
+            }
+    return rt_rccl_try(R->group_end(), "ncclGroupEnd");
+}
 
 // Row bookkeeping for the stripe partition.
 #define RT_MAX_BANDS 8   // row bands of a host-buffer frame on one GPU (rt_api.hip trace_frame_bands)

@@ -2023,8 +2023,8 @@ static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const Rt
 // claim work until the level's queue is empty.  A level of a small part holds a few thousand rays,
 // and launching the full persistent grid for it costs more in block dispatch than the work (8-part
 // probe: 516 -> 564 Mrays/s per GPU with 256 blocks).  The grid is sized from the ray count this
-// level had in a recent frame on this context (L.ctr_hint, copied back asynchronously; -1 before
-// the first one completes: the full grid): up to 8 lanes per ray, 2x headroom, at least 256 blocks
+// level had in a recent frame on this context (L.ctr_hint: the newest copy whose transfer has
+// completed, rt_api.hip prepare; -1 before the first one completes: the full grid): up to 8 lanes per ray, 2x headroom, at least 256 blocks
 // so that a level that grew since keeps a quarter of the chip.  RT_LV_BLOCKS > 0 forces a cap.
 static int level_blocks(const RtLaunch &L, int32_t hint_rays)
 {
@@ -2087,7 +2087,10 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
         }
         launch_persistent(k_cont<3>, st, L, level_blocks(L, L.ctr_hint ? L.ctr_hint[0] : -1));
         // this frame's counters come back for the next frames' grid hints (any recent frame will do)
-        if (L.ctr_hint) HIP_TRY(hipMemcpyAsync(L.ctr_hint, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
+        if (L.ctr_out) {
+            HIP_TRY(hipMemcpyAsync(L.ctr_out, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
+            if (L.ctr_done) HIP_TRY(hipEventRecord((hipEvent_t)L.ctr_done, st));
+        }
     }
     HIP_TRY(hipGetLastError());
     if (ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));

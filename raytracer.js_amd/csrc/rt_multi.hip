@@ -14,6 +14,7 @@
 
 #include <rccl/rccl.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <mutex>
 
@@ -71,8 +72,11 @@ static char g_rccl_err[256] = "";
 const RtRccl *rt_rccl(void)
 {
     std::call_once(g_rccl_once, [] {
-        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        // RT_RCCL_LIB: another library with RCCL's entry points (tests/test_rccl_sequence.py loads a
+        // recording stub through it to check a frame's call sequence without GPUs)
+        const char *lib = getenv("RT_RCCL_LIB");
+        void *h = lib && lib[0] ? dlopen(lib, RTLD_NOW | RTLD_LOCAL) : dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h && !(lib && lib[0])) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
         if (!h) {
             const char *e = dlerror();
             snprintf(g_rccl_err, sizeof g_rccl_err, "dlopen librccl: %s", e ? e : "?");
@@ -98,3 +102,10 @@ const RtRccl *rt_rccl(void)
 }
 
 const char *rt_rccl_error(void) { return g_rccl_err; }
+
+int rt_rccl_try(int rc, const char *what)
+{
+    if (rc == 0) return RT_OK;
+    const RtRccl *R = rt_rccl();
+    return rt_set_error(RT_E_HIP, "%s: RCCL error %d (%s)", what, rc, R ? R->error_string(rc) : "?");
+}

@@ -855,7 +855,18 @@ struct RtSceneStore {
         for (size_t k = 0; k < e.sub_ent.size(); k++)
             if (e.sub_val[k] < -1 || e.sub_val[k] >= nri)
                 return rt_set_error(RT_E_INVALID, "rt_builder_sync: entity %d substance %d", e.sub_ent[k], e.sub_val[k]);
-        // 1. regions of the rebuilt sets (in place when they fit, else at the end of the pools)
+        // 1. regions of the rebuilt sets (in place when they fit, else at the end of the pools).  The
+        // pool check comes first, so that a refused edit (return 1) leaves the store untouched.
+        {
+            size_t lu = list_used, live = list_live;
+            for (size_t k = 0; k < e.set_slot.size(); k++) {
+                const size_t sl = (size_t)e.set_slot[k];
+                const int c = e.set_count[k], cnt = sl < n_old ? slots[sl].cnt : 0, lcap = sl < n_old ? slots[sl].lcap : 0;
+                live += (size_t)c - (size_t)cnt;
+                if (c > lcap) lu += (size_t)(c + c / 2 + 2);
+            }
+            if (lu > 2 * live + 65536) return 1;       // the pools are mostly garbage: compact
+        }
         slots.resize(e.n_slots, Slot{0, 0, 0, 0, 0, -1});
         size_t lu = list_used, bu = bvh_used, live = list_live;
         int moved = 0;
@@ -874,7 +885,6 @@ struct RtSceneStore {
             }
             S.cnt = c;
         }
-        if (lu > 2 * live + 65536) return 1;           // the pools are mostly garbage: compact
         list_used = lu;
         bvh_used = bu;
         list_live = live;
@@ -1046,6 +1056,14 @@ int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, 
 }
 
 uint64_t rt_store_epoch(const RtSceneStore *st) { return st->epoch; }
+
+int rt_store_node_slots(const RtSceneStore *st, int32_t *out, int32_t n)
+{
+    if (!st->has || !st->desc_mirrors) return 1;
+    if ((size_t)n != st->m_order.size()) return -1;
+    memcpy(out, st->m_order.data(), sizeof(int32_t) * (size_t)n);
+    return 0;
+}
 
 int rt_store_apply_edit(RtSceneStore *st, const RtEdit &e, const rt_shade *shades, int32_t n_shades,
                         const double *substance_ri, int32_t n_substances, RtDevScene *dev, rt_update_stats *stats)

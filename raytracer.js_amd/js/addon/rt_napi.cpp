@@ -27,6 +27,7 @@ const char *code_name(int rc)
     case RT_E_FAULT: return "RT_E_FAULT";
     case RT_E_NODEVICE: return "RT_E_NODEVICE";
     case RT_E_TREE: return "RT_E_TREE";
+    case RT_E_STALE: return "RT_E_STALE";
     default: return "RT_E_UNKNOWN";
     }
 }
@@ -197,6 +198,7 @@ napi_value Destroy(napi_env env, napi_callback_info info)
 }
 
 napi_value set_num(napi_env env, napi_value obj, const char *k, double v);
+napi_value update_stats_obj(napi_env env, const rt_update_stats &st);
 
 // uploadScene(ctx, scene) / updateScene(ctx, scene) -> stats: the flattened scene as typed arrays.
 napi_value scene_call(napi_env env, napi_callback_info info, bool update)
@@ -303,6 +305,14 @@ napi_value scene_call(napi_env env, napi_callback_info info, bool update)
     }
     rt_update_stats st;
     if (throw_rc(env, rt_update_scene(ctx, &d, &st))) return nullptr;
+    return update_stats_obj(env, st);
+}
+
+napi_value UploadScene(napi_env env, napi_callback_info info) { return scene_call(env, info, false); }
+napi_value UpdateScene(napi_env env, napi_callback_info info) { return scene_call(env, info, true); }
+
+napi_value update_stats_obj(napi_env env, const rt_update_stats &st)
+{
     napi_value o;
     napi_create_object(env, &o);
     set_num(env, o, "full", st.full);
@@ -316,8 +326,134 @@ napi_value scene_call(napi_env env, napi_callback_info info, bool update)
     return o;
 }
 
-napi_value UploadScene(napi_env env, napi_callback_info info) { return scene_call(env, info, false); }
-napi_value UpdateScene(napi_env env, napi_callback_info info) { return scene_call(env, info, true); }
+// applyEdit(ctx, edit) -> stats, or null when the resident scene cannot take it (RT_E_STALE: the
+// caller uploads in full).  `edit` carries rt_edit_desc's arrays (include/rt.h) as typed arrays and
+// the whole shade / substance tables in uploadScene's form.
+// sceneSlots(ctx, n) -> Int32Array (slot of each DFS id of the last uploaded desc), or null after an edit
+napi_value SceneSlots(napi_env env, napi_callback_info info)
+{
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_TRY(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    if (argc < 2) { napi_throw_error(env, "RT_E_INVALID", "sceneSlots(ctx, n)"); return nullptr; }
+    rt_ctx *ctx = unwrap(env, argv[0]);
+    if (!ctx) return nullptr;
+    int32_t n = 0;
+    NAPI_TRY(napi_get_value_int32(env, argv[1], &n));
+    if (n < 0) { napi_throw_error(env, "RT_E_INVALID", "sceneSlots: n < 0"); return nullptr; }
+    void *data = nullptr;
+    napi_value ab, arr;
+    NAPI_TRY(napi_create_arraybuffer(env, sizeof(int32_t) * (size_t)n, &data, &ab));
+    NAPI_TRY(napi_create_typedarray(env, napi_int32_array, (size_t)n, ab, 0, &arr));
+    const int r = rt_scene_node_slots(ctx, (int32_t *)data, n);
+    if (r == RT_E_STALE) {
+        napi_value nul;
+        napi_get_null(env, &nul);
+        return nul;
+    }
+    if (throw_rc(env, r)) return nullptr;
+    return arr;
+}
+
+napi_value ApplyEdit(napi_env env, napi_callback_info info)
+{
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_TRY(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    if (argc < 2) { napi_throw_error(env, "RT_E_INVALID", "applyEdit(ctx, edit)"); return nullptr; }
+    rt_ctx *ctx = unwrap(env, argv[0]);
+    if (!ctx) return nullptr;
+    napi_value s = argv[1];
+    Typed rs, rc, rch, ru, ss, sb, sc, se, st, ssh, sg, ue, uv, dns, dnv, dsh, sresp, slight, smirror, srough, srgb, simg, ri;
+    if (!get_typed(env, s, "rec_slot", napi_int32_array, rs, true) ||
+        !get_typed(env, s, "rec_cube", napi_float64_array, rc, true) ||
+        !get_typed(env, s, "rec_child", napi_int32_array, rch, true) ||
+        !get_typed(env, s, "rec_up", napi_int32_array, ru, true) ||
+        !get_typed(env, s, "set_slot", napi_int32_array, ss, true) ||
+        !get_typed(env, s, "set_begin", napi_int32_array, sb, true) ||
+        !get_typed(env, s, "set_count", napi_int32_array, sc, true) ||
+        !get_typed(env, s, "set_ent", napi_int32_array, se, true) ||
+        !get_typed(env, s, "set_type", napi_int32_array, st, true) ||
+        !get_typed(env, s, "set_shade", napi_int32_array, ssh, true) ||
+        !get_typed(env, s, "set_geom", napi_float64_array, sg, true) ||
+        !get_typed(env, s, "sub_ent", napi_int32_array, ue, true) ||
+        !get_typed(env, s, "sub_val", napi_int32_array, uv, true) ||
+        !get_typed(env, s, "dfs_new_slot", napi_int32_array, dns, true) ||
+        !get_typed(env, s, "dfs_new_val", napi_int32_array, dnv, true) ||
+        !get_typed(env, s, "dfs_shift", napi_int32_array, dsh, true) ||
+        !get_typed(env, s, "shade_response", napi_int32_array, sresp, true) ||
+        !get_typed(env, s, "shade_light", napi_int32_array, slight, true) ||
+        !get_typed(env, s, "shade_mirror", napi_int32_array, smirror, true) ||
+        !get_typed(env, s, "shade_roughness", napi_float64_array, srough, true) ||
+        !get_typed(env, s, "shade_rgb", napi_float64_array, srgb, true) ||
+        !get_typed(env, s, "shade_image", napi_int32_array, simg, true) ||
+        !get_typed(env, s, "substance_ri", napi_float64_array, ri, true))
+        return nullptr;
+    double n_slots = 0, n_ent = 0, scatter = 0;
+    if (!get_number(env, s, "n_slots", n_slots) || !get_number(env, s, "n_entities", n_ent) ||
+        !get_number(env, s, "scatter", scatter))
+        return nullptr;
+    const size_t nr = rs.length, nset = ss.length, nm = se.length, ns = sresp.length;
+    if (rc.length != 4 * nr || rch.length != 8 * nr || ru.length != 2 * nr || sb.length != nset || sc.length != nset ||
+        st.length != nm || ssh.length != nm || sg.length != 9 * nm || uv.length != ue.length ||
+        dnv.length != dns.length || slight.length != ns || smirror.length != ns || srough.length != ns ||
+        srgb.length != 3 * ns || simg.length != ns) {
+        napi_throw_error(env, "RT_E_INVALID", "applyEdit: inconsistent array lengths");
+        return nullptr;
+    }
+    std::vector<rt_shade> shades(ns);
+    for (size_t i = 0; i < ns; i++) {
+        rt_shade &sh = shades[i];
+        memset(&sh, 0, sizeof sh);
+        sh.response = static_cast<int32_t *>(sresp.data)[i];
+        sh.light = static_cast<int32_t *>(slight.data)[i];
+        sh.mirror = static_cast<int32_t *>(smirror.data)[i];
+        sh.roughness = static_cast<double *>(srough.data)[i];
+        sh.image = static_cast<int32_t *>(simg.data)[i];
+        for (int k = 0; k < 3; k++) sh.rgb[k] = static_cast<double *>(srgb.data)[3 * i + k];
+    }
+    rt_edit_desc d;
+    memset(&d, 0, sizeof d);
+    d.n_slots = (int32_t)n_slots;
+    d.n_entities = (int32_t)n_ent;
+    d.n_rec = (int32_t)nr;
+    d.rec_slot = (const int32_t *)rs.data;
+    d.rec_cube = (const double *)rc.data;
+    d.rec_child = (const int32_t *)rch.data;
+    d.rec_up = (const int32_t *)ru.data;
+    d.n_set = (int32_t)nset;
+    d.set_slot = (const int32_t *)ss.data;
+    d.set_begin = (const int32_t *)sb.data;
+    d.set_count = (const int32_t *)sc.data;
+    d.n_member = (int32_t)nm;
+    d.set_ent = (const int32_t *)se.data;
+    d.set_type = (const int32_t *)st.data;
+    d.set_shade = (const int32_t *)ssh.data;
+    d.set_geom = (const double *)sg.data;
+    d.n_sub = (int32_t)ue.length;
+    d.sub_ent = (const int32_t *)ue.data;
+    d.sub_val = (const int32_t *)uv.data;
+    d.n_dfs_new = (int32_t)dns.length;
+    d.dfs_new_slot = (const int32_t *)dns.data;
+    d.dfs_new_val = (const int32_t *)dnv.data;
+    d.n_dfs_shift = (int32_t)dsh.length;
+    d.dfs_shift = (const int32_t *)dsh.data;
+    d.scatter = scatter != 0;
+    d.n_shades = (int32_t)ns;
+    d.shades = shades.data();
+    d.n_substances = (int32_t)ri.length;
+    d.substance_ri = (const double *)ri.data;
+    rt_update_stats u;
+    memset(&u, 0, sizeof u);
+    const int r = rt_apply_edit(ctx, &d, &u);
+    if (r == RT_E_STALE) {
+        napi_value nul;
+        napi_get_null(env, &nul);
+        return nul;
+    }
+    if (throw_rc(env, r)) return nullptr;
+    return update_stats_obj(env, u);
+}
 
 napi_value set_num(napi_env env, napi_value obj, const char *k, double v)
 {
@@ -446,6 +582,8 @@ napi_value Init(napi_env env, napi_value exports)
         {"destroy", nullptr, Destroy, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"uploadScene", nullptr, UploadScene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"updateScene", nullptr, UpdateScene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"applyEdit", nullptr, ApplyEdit, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"sceneSlots", nullptr, SceneSlots, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"traceFrame", nullptr, TraceFrame, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"lastError", nullptr, LastError, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"abiVersion", nullptr, AbiVersion, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -96,6 +96,18 @@ class rt_exposure_stats(C.Structure):
 RT_TONEMAP_IDENTITY, RT_TONEMAP_STDDEV, RT_TONEMAP_ABSDEV = 0, 1, 2
 
 
+class rt_edit_desc(C.Structure):
+    _P = C.POINTER
+    _fields_ = [("n_slots", _i), ("n_entities", _i), ("n_rec", _i),
+                ("rec_slot", _P(_i)), ("rec_cube", _P(_d)), ("rec_child", _P(_i)), ("rec_up", _P(_i)),
+                ("n_set", _i), ("set_slot", _P(_i)), ("set_begin", _P(_i)), ("set_count", _P(_i)),
+                ("n_member", _i), ("set_ent", _P(_i)), ("set_type", _P(_i)), ("set_shade", _P(_i)),
+                ("set_geom", _P(_d)), ("n_sub", _i), ("sub_ent", _P(_i)), ("sub_val", _P(_i)),
+                ("n_dfs_new", _i), ("n_dfs_shift", _i), ("dfs_new_slot", _P(_i)), ("dfs_new_val", _P(_i)),
+                ("dfs_shift", _P(_i)), ("scatter", _i), ("n_shades", _i), ("n_substances", _i),
+                ("shades", C.c_void_p), ("substance_ri", _P(_d))]
+
+
 class rt_update_stats(C.Structure):
     _fields_ = [("full", _i), ("dirty_nodes", _i), ("new_nodes", _i), ("moved_regions", _i),
                 ("changed_entities", _i), ("pad_", _i), ("bytes", C.c_int64), ("host_ms", _d), ("total_ms", _d)]
@@ -129,7 +141,11 @@ EXPORTS = ("rt_create", "rt_destroy", "rt_last_error", "rt_abi_version", "rt_upl
            "rt_debug_camera_dirs", "rt_builder_create", "rt_builder_destroy", "rt_builder_add",
            "rt_builder_add_many", "rt_builder_desc", "rt_exposure_stats_device", "rt_tonemap_device",
            "rt_tonemap_range", "rt_update_scene", "rt_builder_move", "rt_builder_set_shade",
-           "rt_trace_frame_device", "rt_frame_fault", "rt_ctx_info_get", "rt_builder_sync")
+           "rt_trace_frame_device", "rt_frame_fault", "rt_ctx_info_get", "rt_builder_sync",
+           "rt_debug_rccl_frames", "rt_apply_edit", "rt_scene_node_slots")
+
+# rt_trace_hook: void (*)(int32_t ctx, int32_t device)
+TRACE_HOOK = C.CFUNCTYPE(None, C.c_int32, C.c_int32)
 
 
 def declare(lib):
@@ -149,6 +165,7 @@ def declare(lib):
     lib.rt_kernel_times.argtypes = [vp, _pd, _i]
     lib.rt_debug_walk.argtypes = [vp, _pd, _pd, _i, _i, _pi, _pi, _pi]
     lib.rt_debug_camera_dirs.argtypes = [vp, P(rt_camera_desc), _pd]
+    lib.rt_debug_rccl_frames.argtypes = [_i, _i, _i, _i, _i, _i, _i, _i, TRACE_HOOK]
     lib.rt_builder_create.argtypes = [_pd, _d, P(vp)]
     lib.rt_builder_destroy.argtypes = [vp]
     lib.rt_builder_destroy.restype = None
@@ -159,6 +176,8 @@ def declare(lib):
     lib.rt_tonemap_device.argtypes = [vp, vp, C.c_int64, _d, _d, vp, vp]
     lib.rt_tonemap_range.argtypes = [_i, P(rt_exposure_stats), _i, _d, _d, _pd]
     lib.rt_update_scene.argtypes = [vp, P(rt_scene_desc), P(rt_update_stats)]
+    lib.rt_apply_edit.argtypes = [vp, P(rt_edit_desc), P(rt_update_stats)]
+    lib.rt_scene_node_slots.argtypes = [vp, _pi, _i]
     lib.rt_builder_sync.argtypes = [vp, vp, P(rt_shade), _i, _pd, _i, P(rt_update_stats)]
     lib.rt_builder_move.argtypes = [vp, _i, _pd]
     lib.rt_builder_set_shade.argtypes = [vp, _i, _i, _i]

@@ -1,6 +1,6 @@
 /*
  * run_dropin.js <scene.json> <out_prefix> [--serialize-only] [--scatter <seed>] [--edit A B C]
- *               [--devices 0,0,0] [--repeat N]
+ *               [--devices 0,0,0] [--repeat N] [--plain]
  * Builds reference-shaped objects, checks serialize_scene() reproduces the linearised arrays, and
  * (unless --serialize-only) renders one frame with the drop-in Raytracer into ExposureBuffer.pixels.
  * --scatter: rough mirrors with options.scatter = 'counter', the rng's one draw = seed / 2^53.
@@ -10,6 +10,7 @@
  *   EntitySet, which is where add_entity_to_octree files a cube straddling the centre planes), and
  *   entity B takes entity C's material and texture (set_material / set_texture).
  * --devices: options.devices (one context over several GPUs, or several parts on one GPU).
+ * --plain: options {} (no ids, no counters), the default path a host takes; only pixels are written.
  * --repeat N: after the first frame, N frames timed each with options.stats off, then N with it on
  *   (<out_prefix>.repeat.json).
  */
@@ -58,18 +59,24 @@ const si = process.argv.indexOf('--scatter');
 const seed = si > 0 ? Number(process.argv[si + 1]) : null;
 const rng = seed === null ? null : { next: () => seed / 9007199254740992 };
 const di = process.argv.indexOf('--devices');
-const opts = seed === null ? { keep_ids: true, stats: true } : { keep_ids: true, stats: true, scatter: 'counter' };
+// --plain: the reference's trace_frame() as a host calls it (no ids, no counters: the split passes
+// and, from RT_BAND_MIN pixels, row bands); only the pixels are written
+const plain = process.argv.includes('--plain');
+const opts = plain ? {} : { keep_ids: true, stats: true };
+if (seed !== null) opts.scatter = 'counter';
 if (di > 0) opts.devices = process.argv[di + 1].split(',').map(Number);
 const tracer = new rt.Raytracer(config, world.root, cam, eb, rng, opts);
 const t0 = process.hrtime.bigint();
 tracer.trace_frame();
 const t1 = process.hrtime.bigint();
 assert.strictEqual(eb.cleaned, 1);
-const ids = Int32Array.from(tracer.last_hit_entity, (i) => (i >= 0 ? tracer._scene.entities[i].__orig_id : i));
 fs.writeFileSync(out_prefix + '.rgb', Buffer.from(eb.pixels.buffer));
-fs.writeFileSync(out_prefix + '.ent', Buffer.from(ids.buffer));
-fs.writeFileSync(out_prefix + '.node', Buffer.from(tracer.last_hit_node.buffer));
-fs.writeFileSync(out_prefix + '.status', Buffer.from(tracer.last_status.buffer));
+if (!plain) {
+	const ids = Int32Array.from(tracer.last_hit_entity, (i) => (i >= 0 ? tracer._scene.entities[i].__orig_id : i));
+	fs.writeFileSync(out_prefix + '.ent', Buffer.from(ids.buffer));
+	fs.writeFileSync(out_prefix + '.node', Buffer.from(tracer.last_hit_node.buffer));
+	fs.writeFileSync(out_prefix + '.status', Buffer.from(tracer.last_status.buffer));
+}
 fs.writeFileSync(out_prefix + '.json', JSON.stringify({ stats: tracer.last_stats, wall_ms: Number(t1 - t0) / 1e6 }));
 
 function write_frame(prefix, extra) {
@@ -96,8 +103,8 @@ if (ri > 0) {
 		}
 		return ms;
 	};
-	const plain = times(false), counted = times(true);
-	fs.writeFileSync(out_prefix + '.repeat.json', JSON.stringify({ frame_ms: plain, frame_ms_stats: counted }));
+	const ms_plain = times(false), ms_counted = times(true);
+	fs.writeFileSync(out_prefix + '.repeat.json', JSON.stringify({ frame_ms: ms_plain, frame_ms_stats: ms_counted }));
 }
 
 const ei = process.argv.indexOf('--edit');

@@ -40,7 +40,9 @@ def test_struct_layouts_match_header(tmp_path):
                     'sizeof(rt_stats),sizeof(rt_create_desc),sizeof(rt_entity_in),offsetof(rt_scene_desc,substance_ri),'
                     'sizeof(rt_exposure_stats),sizeof(rt_image_desc),offsetof(rt_scene_desc,images),'
                     'sizeof(rt_update_stats),offsetof(rt_config_desc,sky_image),sizeof(rt_ctx_info),'
-                    'offsetof(rt_create_desc,devices));return 0;}\n')
+                    'offsetof(rt_create_desc,devices));'
+                    'printf("%zu %zu %zu\\n",sizeof(rt_edit_desc),offsetof(rt_edit_desc,scatter),'
+                    'offsetof(rt_edit_desc,substance_ri));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
@@ -48,7 +50,8 @@ def test_struct_layouts_match_header(tmp_path):
             C.sizeof(abi.rt_config_desc), C.sizeof(abi.rt_stats), C.sizeof(abi.rt_create_desc),
             C.sizeof(abi.rt_entity_in), abi.rt_scene_desc.substance_ri.offset, C.sizeof(abi.rt_exposure_stats),
             C.sizeof(abi.rt_image_desc), abi.rt_scene_desc.images.offset, C.sizeof(abi.rt_update_stats),
-            abi.rt_config_desc.sky_image.offset, C.sizeof(abi.rt_ctx_info), abi.rt_create_desc.devices.offset]
+            abi.rt_config_desc.sky_image.offset, C.sizeof(abi.rt_ctx_info), abi.rt_create_desc.devices.offset,
+            C.sizeof(abi.rt_edit_desc), abi.rt_edit_desc.scatter.offset, abi.rt_edit_desc.substance_ri.offset]
     assert got == want
 
 

@@ -112,6 +112,34 @@ def test_dropin_frame_equals_oracle(tmp_path, name, wh, refmax, devices):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name,wh,band_min", [("config1", (256, 256), None), ("small4", (200, 150), "0"),
+                                              ("config1", (256, 256), "0"), ("small4_rough", (200, 150), "0")])
+def test_dropin_default_options_frame_equals_oracle(tmp_path, name, wh, band_min):
+    """The drop-in as a host calls it: trace_frame() with options {} (no ids, no counters), i.e. the
+    split passes without the counting kernel, and with RT_BAND_MIN=0 the frame as row bands on their
+    own streams (the path 1080p-and-up frames take).  Pixels equal the oracle bit for bit."""
+    spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4),
+            "small4_rough": lambda: scenes.roughen(scenes.small_random(4, p_mirror=0.5))}[name]()
+    seed = 123456789012345 if name.endswith("rough") else None
+    cam = scenes.make_camera(*wh)
+    cfg = scenes.make_config(3, scatter_seed=seed)
+    path = _dump(tmp_path, spec, cam, cfg)
+    env = dict(os.environ)
+    if band_min is not None:
+        env["RT_BAND_MIN"] = band_min
+    r = subprocess.run([NODE, RUNNER, path, str(tmp_path / "out"), "--plain"] + (["--scatter", str(seed)] if seed else []),
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert not (tmp_path / "out.ent").exists()
+    rgb = np.fromfile(tmp_path / "out.rgb", dtype=np.float32)
+    w, root = oracle.build_scene(spec)
+    ref = w.trace_frame(root, cam, cfg, nthreads=8)
+    assert np.array_equal(rgb.view(np.uint32), ref["rgb"].view(np.uint32))
+    st = json.loads((tmp_path / "out.json").read_text())["stats"]
+    assert "frame_ms" in st and "segments" not in st, st          # no counters: the split passes ran
+
+
+@pytest.mark.gpu
 def test_dropin_scene_edit_updates_incrementally(tmp_path):
     """invalidate_scene() after editing the live scene: the second frame comes from rt_update_scene
     (stable ids from serialize_scene(prev)) and equals the oracle after the same edits."""
