@@ -398,9 +398,10 @@ int  rt_builder_sync(rt_ctx *ctx, rt_builder *b, const rt_shade *shades, int32_t
                      const double *substance_ri, int32_t n_substances, rt_update_stats *stats);
 
 /* ---- O(edit) scene updates from a host that journals its own edits (the JS drop-in) ---- */
-/* The edit of the resident scene since the last rt_upload_scene / rt_update_scene(full) /
- * rt_apply_edit on ctx, in the resident scene's node slots: a full upload numbers the slots in DFS
- * order (slot k = DFS id k of that upload) and every later node takes the next slot.  The host names
+/* The edit of the resident scene since the last rt_upload_scene / rt_update_scene / rt_apply_edit on
+ * ctx, in the resident scene's node slots: rt_scene_node_slots gives the slot of every node of the
+ * last uploaded desc (DFS order after a full upload unless RT_TOP_LEVELS is set), and every node
+ * created since takes the next slot.  The host names
  * what changed (the same content rt_builder_sync derives from the native builder's journal):
  *   rec_*:  node records to (re)write, ascending slots: every new node, and existing nodes that
  *           gained a child (cube pos.xyz + size, 8 child slots with -1 empty, parent slot with -1
@@ -443,12 +444,13 @@ typedef struct rt_edit_desc {
 } rt_edit_desc;
 int  rt_apply_edit(rt_ctx *ctx, const rt_edit_desc *edit, rt_update_stats *stats);
 
-/* The resident node slot of each DFS id (out[k] = slot of the scene desc's node k) after the last
- * rt_upload_scene / rt_update_scene, for a host that journals edits in slots (rt_apply_edit): a full
- * upload numbers slots in DFS order, an incremental rt_update_scene keeps old nodes in their slots.
- * n = the desc's node count.  RT_E_STALE after an rt_apply_edit / rt_builder_sync edit (the map is
- * the host's own then).  Replaces no reference interface. */
-int  rt_scene_node_slots(rt_ctx *ctx, int32_t *out, int32_t n);
+/* The resident node slot of each DFS id (out[k] = slot of the scene desc's node k) and the number of
+ * slots (*n_slots; slots of nodes that left the tree stay allocated) after the last rt_upload_scene /
+ * rt_update_scene, for a host that journals edits in slots (rt_apply_edit): a full upload numbers
+ * slots in DFS order, an incremental rt_update_scene keeps old nodes in their slots.  n = the desc's
+ * node count.  RT_E_STALE after an rt_apply_edit / rt_builder_sync edit (the map is the host's own
+ * then).  Replaces no reference interface. */
+int  rt_scene_node_slots(rt_ctx *ctx, int32_t *out, int32_t n, int32_t *n_slots);
 
 #ifdef __cplusplus
 }

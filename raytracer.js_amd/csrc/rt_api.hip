@@ -363,7 +363,7 @@ extern "C" int rt_builder_sync(rt_ctx *c, rt_builder *b, const rt_shade *shades,
                 for (int k = 0; k < c->n_dev; k++) c->dev[k].scene = scenes[k];
                 c->scatter = e.scatter;
                 c->has_scene = true;
-                rt_builder_synced(b, c->store, rt_store_epoch(c->store), false);
+                rt_builder_synced(b, c->store, rt_store_epoch(c->store), false, nullptr);
                 return RT_OK;
             }
         }
@@ -375,7 +375,7 @@ extern "C" int rt_builder_sync(rt_ctx *c, rt_builder *b, const rt_shade *shades,
     r = upload(c, &d, false, stats);
     if (r != RT_OK) return r;
     if (stats) stats->full = 1;
-    rt_builder_synced(b, c->store, rt_store_epoch(c->store), true);
+    rt_builder_synced(b, c->store, rt_store_epoch(c->store), true, rt_store_order(c->store));
     return RT_OK;
 }
 
@@ -455,11 +455,11 @@ extern "C" int rt_apply_edit(rt_ctx *c, const rt_edit_desc *d, rt_update_stats *
     return RT_OK;
 }
 
-extern "C" int rt_scene_node_slots(rt_ctx *c, int32_t *out, int32_t n)
+extern "C" int rt_scene_node_slots(rt_ctx *c, int32_t *out, int32_t n, int32_t *n_slots)
 {
-    if (!c || !out || n < 0) return rt_set_error(RT_E_INVALID, "rt_scene_node_slots: bad argument");
+    if (!c || !out || n < 0 || !n_slots) return rt_set_error(RT_E_INVALID, "rt_scene_node_slots: bad argument");
     if (!c->has_scene) return rt_set_error(RT_E_NOSCENE, "rt_scene_node_slots: no scene uploaded");
-    const int r = rt_store_node_slots(c->store, out, n);
+    const int r = rt_store_node_slots(c->store, out, n, n_slots);
     if (r < 0) return rt_set_error(RT_E_INVALID, "rt_scene_node_slots: n = %d is not the node count", n);
     if (r > 0) return rt_set_error(RT_E_STALE, "rt_scene_node_slots: the resident scene was edited since its desc");
     return RT_OK;

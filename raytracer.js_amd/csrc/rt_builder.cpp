@@ -528,11 +528,11 @@ int rt_builder_edit(rt_builder *b, const RtSceneStore *st, uint64_t epoch, const
     return 0;
 }
 
-void rt_builder_synced(rt_builder *b, const RtSceneStore *st, uint64_t epoch, bool full)
+void rt_builder_synced(rt_builder *b, const RtSceneStore *st, uint64_t epoch, bool full, const int32_t *order)
 {
-    if (full) {                                  // a full upload numbers the slots in DFS order
+    if (full) {                                  // the full upload's slot of each DFS id (DFS order by default)
         b->slot.assign(b->nodes.size(), -1);
-        for (size_t k = 0; k < b->l_order.size(); k++) b->slot[b->l_order[k]] = (int32_t)k;
+        for (size_t k = 0; k < b->l_order.size(); k++) b->slot[b->l_order[k]] = order ? order[k] : (int32_t)k;
         b->unreached = b->nodes.size() - b->l_order.size();
         // subtree sizes of the reachable tree (a replaced child leaves its old subtree counted)
         b->sub.assign(b->nodes.size(), 0);

@@ -90,6 +90,8 @@ struct RtDevScene {
     int32_t n_nodes, n_list, n_entities, n_shades, n_subs, n_bvh, n_images;
     int32_t exact_slots;        // every node's slot planes equal its slot positions (dyadic cubes): the
                                 // walker takes them without recomputing the Box centre (rt_kernels.hip)
+    int32_t n_top;              // slots [0, n_top) hold the upper levels breadth-first (RT_TOP_LEVELS; else 0)
+    int32_t n_lds;              // walk kernels: slots [0, n_lds) are read from the workgroup's LDS copy
 };
 
 // A ray of the split path at its first continuation (segment start after a mirror / transmission
@@ -124,9 +126,11 @@ int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, 
 // Every upload / update / edit of a store bumps its epoch: a builder's journal is only valid
 // against the store state it was synced with.
 uint64_t rt_store_epoch(const RtSceneStore *st);
-// The slot of each DFS id of the last uploaded desc (0; 1 when the mirrors are not kept, i.e. after
-// an edit; -1 when n is not the node count).
-int rt_store_node_slots(const RtSceneStore *st, int32_t *out, int32_t n);
+// The slot of each DFS id of the last uploaded desc and the slot count (0; 1 when the mirrors are
+// not kept, i.e. after an edit; -1 when n is not the node count).
+int rt_store_node_slots(const RtSceneStore *st, int32_t *out, int32_t n, int32_t *n_slots);
+// The slot of each DFS id of the last uploaded desc, or null after an edit.
+const int32_t *rt_store_order(const RtSceneStore *st);
 
 // An edit of the resident scene made through the native builder since its last rt_builder_sync
 // (rt_builder.cpp builds it from the builder's journal, rt_scene.hip applies it): O(edit) on the
@@ -153,8 +157,9 @@ struct RtEdit {
 // (never synced with this store state, or an edit the journal cannot express).
 int rt_builder_edit(rt_builder *b, const RtSceneStore *st, uint64_t epoch, const rt_shade *shades, int32_t n_shades,
                     RtEdit &out);
-// After a successful sync: `full` = the scene went up through rt_builder_desc + a full upload.
-void rt_builder_synced(rt_builder *b, const RtSceneStore *st, uint64_t epoch, bool full);
+// After a successful sync: `full` = the scene went up through rt_builder_desc + a full upload, whose
+// slot of each DFS id is order[] (rt_store_order).
+void rt_builder_synced(rt_builder *b, const RtSceneStore *st, uint64_t epoch, bool full, const int32_t *order);
 // RT_OK, 1 (a full upload is needed: the pools are mostly garbage), or an error.
 int rt_store_apply_edit(RtSceneStore *st, const RtEdit &e, const rt_shade *shades, int32_t n_shades,
                         const double *substance_ri, int32_t n_substances, RtDevScene *dev, rt_update_stats *stats);

@@ -47,19 +47,57 @@ __device__ __forceinline__ T ld_at(const void *base, uint32_t off)
 __device__ __forceinline__ uint32_t node_off(int n) { return (uint32_t)n << 7; }
 enum : uint32_t { NODE_CHILD = 32, NODE_BOX = 64, NODE_NENT = 96, NODE_UP = 112 };
 
+// LDS staging of the upper octree levels (build with -DRT_LDS_TOP=K, scene uploaded
+// with RT_TOP_LEVELS): a walk kernel copies node slots [0, S.n_lds) — the levels every ray crosses,
+// breadth-first — into its workgroup's LDS once, and node reads of those slots are served there.
+// S.n_lds is min(n_top, K) for the walk kernels' launches and 0 for every other kernel.
+// The copy lives in dynamic LDS (S.n_lds * 128 bytes, given at the walk kernels' launches), so no
+// other kernel's occupancy pays for it.
+#ifndef RT_LDS_TOP
+#define RT_LDS_TOP 0
+#endif
+#if RT_LDS_TOP
+extern __shared__ RtNode s_top[];
+#endif
+
+template <typename T>
+__device__ __forceinline__ T ld_node(const RtDevScene &S, int n, uint32_t field)
+{
+#if RT_LDS_TOP
+    if ((unsigned)n < (unsigned)S.n_lds)
+        return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(s_top) + node_off(n) + field);
+#endif
+    return ld_at<T>(S.node, node_off(n) + field);
+}
+
+// a walk kernel's prologue: the workgroup's copy of slots [0, S.n_lds)
+__device__ __forceinline__ void stage_top(const RtDevScene &S)
+{
+#if RT_LDS_TOP
+    if (S.n_lds > 0) {
+        const int4 *src = reinterpret_cast<const int4 *>(S.node);
+        int4 *dst = reinterpret_cast<int4 *>(s_top);
+        for (int i = threadIdx.x; i < S.n_lds * 8; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+#else
+    (void)S;
+#endif
+}
+
 __device__ __forceinline__ NodeDims node_dims(const RtDevScene &S, int n)
 {
-    const double4 v = ld_at<double4>(S.node, node_off(n));
+    const double4 v = ld_node<double4>(S, n, 0);
     return {v.x, v.y, v.z, v.w};
 }
 
 __device__ __forceinline__ int node_child(const RtDevScene &S, int n, int oct)
 {
-    return ld_at<int32_t>(S.node, node_off(n) + NODE_CHILD + ((uint32_t)oct << 2));
+    return ld_node<int32_t>(S, n, NODE_CHILD + ((uint32_t)oct << 2));
 }
 
 // {up_tree, up_oct, up2_tree, up2_oct} of node n (one 16-byte load)
-__device__ __forceinline__ int4 node_up4(const RtDevScene &S, int n) { return ld_at<int4>(S.node, node_off(n) + NODE_UP); }
+__device__ __forceinline__ int4 node_up4(const RtDevScene &S, int n) { return ld_node<int4>(S, n, NODE_UP); }
 
 // The walk pass's candidate filter of a returned node: it has entities and (culling on, finite ray)
 // the ray crosses its cull-hierarchy root box.  One line: count and box.
@@ -843,11 +881,10 @@ __device__ __forceinline__ bool ray_box(const RtBvh &b, const RayBox &rb)
 
 __device__ __forceinline__ bool node_candidate(const RtDevScene &S, int n, bool cull, const RayBox &rb)
 {
-    const uint32_t off = node_off(n);
-    if (ld_at<int32_t>(S.node, off + NODE_NENT) == 0) return false;
+    if (ld_node<int32_t>(S, n, NODE_NENT) == 0) return false;
     if (!cull || !rb.ok) return true;
-    const float4 lo = ld_at<float4>(S.node, off + NODE_BOX);        // lo.xyz, hi.x
-    const float2 hi = ld_at<float2>(S.node, off + NODE_BOX + 16);   // hi.yz
+    const float4 lo = ld_node<float4>(S, n, NODE_BOX);              // lo.xyz, hi.x
+    const float2 hi = ld_node<float2>(S, n, NODE_BOX + 16);         // hi.yz
     RtBvh b;
     b.lo[0] = lo.x; b.lo[1] = lo.y; b.lo[2] = lo.z;
     b.hi[0] = lo.w; b.hi[1] = hi.x; b.hi[2] = hi.y;
@@ -1547,6 +1584,7 @@ template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
 {
     if (!seg_mode(L)) return;
+    stage_top(L.scene);
     const int lane = threadIdx.x & 63;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const RtDevScene &S = L.scene;
@@ -1690,6 +1728,7 @@ template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
 {
     if (!refill_level(L)) return;
+    stage_top(L.scene);
     constexpr int IDLE = 9;
     const int lane = threadIdx.x & 63;
     const RtDevScene &S = L.scene;
@@ -1750,6 +1789,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (seg_mode(L) || refill_level(L)) return;       // k_walk_seg / k_walk_refill take this level
+    stage_top(S);
     for (;;) {
         int t_end;
         const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
@@ -1991,12 +2031,14 @@ __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, doub
 // makes an over-estimate harmless (late blocks find the queue empty).  The CU count and each
 // kernel's blocks per CU are queried once (all devices of a context are MI355X): one host thread
 // issues the launches of up to 8 GPUs, so a launch is only the launch.
-static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const RtLaunch &L, int max_blocks = 0)
+static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const RtLaunch &L, int max_blocks = 0,
+                              size_t lds = 0)
 {
     static std::atomic<int> cus{0};
     static std::mutex mu;
-    static std::vector<std::pair<const void *, int>> per_kernel;
+    static std::vector<std::pair<std::pair<const void *, size_t>, int>> per_kernel;
     const void *kp = reinterpret_cast<const void *>(kernel);
+    const std::pair<const void *, size_t> key(kp, lds);
     int n_cu = cus.load(std::memory_order_relaxed), per = 0;
     {
         std::lock_guard<std::mutex> g(mu);
@@ -2008,15 +2050,15 @@ static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const Rt
             cus.store(n_cu);
         }
         for (const auto &e : per_kernel)
-            if (e.first == kp) per = e.second;
+            if (e.first == key) per = e.second;
         if (!per) {
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kp, 256, 0) != hipSuccess || per < 1) per = 1;
-            per_kernel.emplace_back(kp, per);
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kp, 256, lds) != hipSuccess || per < 1) per = 1;
+            per_kernel.emplace_back(key, per);
         }
     }
     int nb = n_cu * per;
     if (max_blocks > 0 && nb > max_blocks) nb = max_blocks;
-    hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), 0, st, L);
+    hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, st, L);
 }
 
 // Grid of a bounce-level pass (or k_cont).  Persistent passes are correct at any grid size: waves
@@ -2074,11 +2116,14 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             // per-lane refill only where a recent frame had a wide level (both walk kernels read Lv.refill)
             Lv.refill = L.refill_always || hint > 64 * 4096 ? L.refill : 0;
             if (lv == 0 && walk_wait) HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)walk_wait, 0));
-            launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lv, mb);
+            RtLaunch Lw = Lv;                         // the walk kernels read the upper levels from LDS
+            Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
+            const size_t lds = sizeof(RtNode) * (size_t)Lw.scene.n_lds;
+            launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb, lds);
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
-            if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lv, mb);     // one of the two runs (§5.10)
-            if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<4>, st, Lv, mb);
+            if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lw, mb, lds);   // one of the two runs (§5.10)
+            if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<4>, st, Lw, mb, lds);
             launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
             if (lv >= 1 && L.seg > 1) launch_persistent(k_first_seg<4>, st, Lv, mb);

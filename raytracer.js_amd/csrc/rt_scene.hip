@@ -300,6 +300,10 @@ struct RtSceneStore {
         nd.up2_oct = nd.up_tree >= 0 ? m_up[2 * (size_t)nd.up_tree + 1] : RT_OCT_UNDEF;
     }
     std::vector<int32_t> m_order;                      // slot of each DFS id
+    // RT_TOP_LEVELS = D > 0: a full upload gives the nodes of depth <= D the first slots, in
+    // breadth-first order (n_top of them), so the walk kernels can stage them in LDS
+    int top_levels = 0;
+    int32_t n_top = 0;
     std::vector<int32_t> m_list;                       // 1 / list-pool entry
     std::vector<int32_t> m_type, m_shade, m_sub;       // 1 / entity
     std::vector<double> m_geom;                        // 9 / entity
@@ -498,6 +502,8 @@ struct RtSceneStore {
         d.n_shades = n_shades;
         d.n_subs = n_subs;
         d.n_bvh = (int32_t)bvh_used;
+        d.n_top = n_top;
+        d.n_lds = 0;                                   // set per launch for the walk kernels (rt_kernels.hip)
 #ifdef RT_NO_EXACT_SLOTS
         d.exact_slots = 0;                             // A/B builds: the general plane computation only
 #else
@@ -526,7 +532,51 @@ struct RtSceneStore {
         return w;
     }
 
-    // Full upload: slots in DFS order, regions packed exactly.
+    // Upper levels first (top_levels = D > 0): the nodes of depth <= D move to slots 0..n_top-1 in
+    // breadth-first order (the root stays slot 0), every other node follows in DFS order.  Applied to
+    // the DFS-slot arrays full() just built: records (children, parent and grandparent links
+    // renumbered), parent links, entity ranges, region slots, node_dfs / m_order and the cube map.
+    void permute_top(const rt_scene_desc *s)
+    {
+        const int N = s->n_nodes;
+        std::vector<int32_t> depth(N, 0), perm(N);
+        for (int n = 1; n < N; n++) depth[n] = depth[s->node_parent[n]] + 1;     // DFS: parents first
+        int32_t k = 0;
+        for (int d = 0; d <= top_levels; d++)
+            for (int n = 0; n < N; n++)
+                if (depth[n] == d) perm[n] = k++;
+        n_top = k;
+        for (int n = 0; n < N; n++)
+            if (depth[n] > top_levels) perm[n] = k++;
+        auto re = [&](int32_t x) { return x >= 0 ? perm[x] : x; };
+        std::vector<RtNode> nn(N);
+        std::vector<int32_t> nu(2 * (size_t)N), ne(4 * (size_t)N);
+        std::vector<Slot> ns(N);
+        std::vector<uint8_t> ni(N);
+        for (int n = 0; n < N; n++) {
+            const int p = perm[n];
+            RtNode nd = m_node[n];
+            for (int c = 0; c < 8; c++) nd.child[c] = re(nd.child[c]);
+            nd.up_tree = re(nd.up_tree);
+            nd.up2_tree = re(nd.up2_tree);
+            nn[p] = nd;
+            nu[2 * (size_t)p] = re(m_up[2 * (size_t)n]);
+            nu[2 * (size_t)p + 1] = m_up[2 * (size_t)n + 1];
+            for (int j = 0; j < 4; j++) ne[4 * (size_t)p + j] = m_ent[4 * (size_t)n + j];
+            ns[p] = slots[n];
+            ni[p] = m_inexact[n];
+            m_dfs[p] = n;
+            m_order[n] = p;
+        }
+        m_node.swap(nn);
+        m_up.swap(nu);
+        m_ent.swap(ne);
+        slots.swap(ns);
+        m_inexact.swap(ni);
+        for (auto &kv : slot_of) kv.second = perm[kv.second];
+    }
+
+    // Full upload: slots in DFS order (upper levels first with top_levels), regions packed exactly.
     int full(const rt_scene_desc *s, const std::vector<int32_t> &oct, rt_update_stats &us)
     {
         const int N = s->n_nodes, NL = s->n_list;
@@ -589,6 +639,8 @@ struct RtSceneStore {
             bb += c ? 2 * (size_t)c - 1 : 0;
         }
         if ((int)slot_of.size() != N) return rt_set_error(RT_E_INVALID, "rt_upload_scene: two nodes share a cube");
+        n_top = 0;
+        if (top_levels > 0) permute_top(s);
         list_used = lb;
         bvh_used = bb;
         entity_mirrors(s);
@@ -1010,6 +1062,7 @@ RtSceneStore *rt_store_new(bool sah, int ndev, const int *devs, void *const *str
     if (!st) return nullptr;
     st->sah = sah;
     st->ndev = ndev;
+    if (const char *e = getenv("RT_TOP_LEVELS")) st->top_levels = atoi(e) < 0 ? 0 : (atoi(e) > 8 ? 8 : atoi(e));
     for (int k = 0; k < ndev; k++) {
         st->devs[k] = devs[k];
         st->sts[k] = (hipStream_t)streams[k];
@@ -1057,11 +1110,17 @@ int rt_store_upload(RtSceneStore *st, const rt_scene_desc *s, bool incremental, 
 
 uint64_t rt_store_epoch(const RtSceneStore *st) { return st->epoch; }
 
-int rt_store_node_slots(const RtSceneStore *st, int32_t *out, int32_t n)
+const int32_t *rt_store_order(const RtSceneStore *st)
+{
+    return st->has && st->desc_mirrors ? st->m_order.data() : nullptr;
+}
+
+int rt_store_node_slots(const RtSceneStore *st, int32_t *out, int32_t n, int32_t *n_slots)
 {
     if (!st->has || !st->desc_mirrors) return 1;
     if ((size_t)n != st->m_order.size()) return -1;
     memcpy(out, st->m_order.data(), sizeof(int32_t) * (size_t)n);
+    *n_slots = (int32_t)st->slots.size();
     return 0;
 }
 

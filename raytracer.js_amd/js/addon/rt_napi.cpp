@@ -329,7 +329,8 @@ napi_value update_stats_obj(napi_env env, const rt_update_stats &st)
 // applyEdit(ctx, edit) -> stats, or null when the resident scene cannot take it (RT_E_STALE: the
 // caller uploads in full).  `edit` carries rt_edit_desc's arrays (include/rt.h) as typed arrays and
 // the whole shade / substance tables in uploadScene's form.
-// sceneSlots(ctx, n) -> Int32Array (slot of each DFS id of the last uploaded desc), or null after an edit
+// sceneSlots(ctx, n) -> {slots: Int32Array (slot of each DFS id of the last uploaded desc), n_slots},
+// or null after an edit
 napi_value SceneSlots(napi_env env, napi_callback_info info)
 {
     size_t argc = 2;
@@ -345,14 +346,19 @@ napi_value SceneSlots(napi_env env, napi_callback_info info)
     napi_value ab, arr;
     NAPI_TRY(napi_create_arraybuffer(env, sizeof(int32_t) * (size_t)n, &data, &ab));
     NAPI_TRY(napi_create_typedarray(env, napi_int32_array, (size_t)n, ab, 0, &arr));
-    const int r = rt_scene_node_slots(ctx, (int32_t *)data, n);
+    int32_t n_slots = 0;
+    const int r = rt_scene_node_slots(ctx, (int32_t *)data, n, &n_slots);
     if (r == RT_E_STALE) {
         napi_value nul;
         napi_get_null(env, &nul);
         return nul;
     }
     if (throw_rc(env, r)) return nullptr;
-    return arr;
+    napi_value o;
+    napi_create_object(env, &o);
+    NAPI_TRY(napi_set_named_property(env, o, "slots", arr));
+    set_num(env, o, "n_slots", n_slots);
+    return o;
 }
 
 napi_value ApplyEdit(napi_env env, napi_callback_info info)

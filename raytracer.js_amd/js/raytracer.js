@@ -165,7 +165,6 @@ function serialize_scene(otree, default_substance, prev, sky_texture) {
 		}
 		node_ent_count[k] = cnt;
 	}
-	for (const t of nodes) delete t.__rt_id;
 
 	const ne = entities.length;
 	const ent_type = new Int32Array(ne), ent_geom = new Float64Array(9 * ne);
@@ -173,68 +172,301 @@ function serialize_scene(otree, default_substance, prev, sky_texture) {
 	const shades = prev ? prev._maps.shades.slice() : [];
 	const shade_index = new Map();
 	if (prev) for (const [m, per] of prev._maps.shade_index) shade_index.set(m, new Map(per));
+	for (const t of nodes) delete t.__rt_id;
 	for (let i = 0; i < ne; i++) {
 		const e = entities[i];
-		const kind = entity_kind(e);
-		ent_type[i] = kind;
-		const g = ent_geom.subarray(9 * i, 9 * i + 9);
-		if (kind === RT_ENT_SPHERE) {
-			const pos = vec(e.get_pos());
-			const d = e.get_diameter();
-			const sm = e.sphere_math || {};
-			g[0] = pos[0]; g[1] = pos[1]; g[2] = pos[2]; g[3] = d;
-			// caches exactly as the reference holds them (src/entities/entity_sphere.ts:34-39,
-			// src/math/intersection.ts:94-97)
-			g[4] = sm._dot_pp !== undefined ? sm._dot_pp : ((0 + pos[0] * pos[0]) + pos[1] * pos[1]) + pos[2] * pos[2];
-			g[5] = sm._radius_sq !== undefined ? sm._radius_sq : (d / 2) * (d / 2);
-			g[6] = e._radius_sq !== undefined ? e._radius_sq : d * d / 4;
-		} else if (kind === RT_ENT_BOX) {
-			const pos = vec(e.get_pos());
-			g[0] = pos[0]; g[1] = pos[1]; g[2] = pos[2]; g[3] = e.get_size();
-		} else {
-			const vs = e.get_vertices();
-			for (let j = 0; j < 3; j++) {
-				const v = vec(vs[j]);
-				g[3 * j] = v[0]; g[3 * j + 1] = v[1]; g[3 * j + 2] = v[2];
-			}
-		}
-		const m = e.get_material(), tex = e.get_texture();
-		let per_mat = shade_index.get(m);
-		if (!per_mat) { per_mat = new Map(); shade_index.set(m, per_mat); }
-		if (!per_mat.has(tex)) {
-			per_mat.set(tex, shades.length);
-			shades.push(null);
-		}
-		ent_shade[i] = per_mat.get(tex);
+		ent_type[i] = entity_geom(e, ent_geom.subarray(9 * i, 9 * i + 9));
+		ent_shade[i] = shade_row(shade_index, shades, e);
 		ent_substance[i] = sub_of(e.get_substance());
 	}
-	// every (material, texture) row is re-read: a host may have edited a material in place
+	const tables = shade_tables(shades, shade_index, image_of);
+	const sky_image = image_of(sky_texture);
+	const def_sub = sub_of(default_substance);
+	const substance_ri = new Float64Array(substances.map((s) => s.refractive_index));
+	return Object.assign({
+		node_pos, node_size, node_parent, node_child, node_ent_begin, node_ent_count,
+		list_entity: new Int32Array(list), ent_type, ent_geom, ent_shade, ent_substance, substance_ri,
+		images: images.map((t) => ({ width: t.width, height: t.height, rgb: image_bytes(t) })),
+		entities, substances, default_substance_index: def_sub, sky_image,
+		_maps: { ent_index, sub_index, shades, shade_index, images, image_index, sub_of },
+		_nodes: nodes
+	}, tables);
+}
+
+/** rt_scene_desc's ent_type / ent_geom record of entity e: its RT_ENT_* kind, geometry into g[0..8]. */
+function entity_geom(e, g) {
+	const kind = entity_kind(e);
+	if (kind === RT_ENT_SPHERE) {
+		const pos = vec(e.get_pos());
+		const d = e.get_diameter();
+		const sm = e.sphere_math || {};
+		g[0] = pos[0]; g[1] = pos[1]; g[2] = pos[2]; g[3] = d;
+		// caches exactly as the reference holds them (src/entities/entity_sphere.ts:34-39,
+		// src/math/intersection.ts:94-97)
+		g[4] = sm._dot_pp !== undefined ? sm._dot_pp : ((0 + pos[0] * pos[0]) + pos[1] * pos[1]) + pos[2] * pos[2];
+		g[5] = sm._radius_sq !== undefined ? sm._radius_sq : (d / 2) * (d / 2);
+		g[6] = e._radius_sq !== undefined ? e._radius_sq : d * d / 4;
+	} else if (kind === RT_ENT_BOX) {
+		const pos = vec(e.get_pos());
+		g[0] = pos[0]; g[1] = pos[1]; g[2] = pos[2]; g[3] = e.get_size();
+	} else {
+		const vs = e.get_vertices();
+		for (let j = 0; j < 3; j++) {
+			const v = vec(vs[j]);
+			g[3 * j] = v[0]; g[3 * j + 1] = v[1]; g[3 * j + 2] = v[2];
+		}
+	}
+	return kind;
+}
+
+/** The shade row of e's (material, texture) pair; a new pair gets the next row (filled by shade_tables). */
+function shade_row(shade_index, shades, e) {
+	const m = e.get_material(), tex = e.get_texture();
+	let per_mat = shade_index.get(m);
+	if (!per_mat) { per_mat = new Map(); shade_index.set(m, per_mat); }
+	if (!per_mat.has(tex)) {
+		per_mat.set(tex, shades.length);
+		shades.push(null);
+	}
+	return per_mat.get(tex);
+}
+
+/** Every (material, texture) row re-read (a host may have edited a material in place), as the
+ * shade_* arrays of rt_scene_desc. */
+function shade_tables(shades, shade_index, image_of) {
 	for (const [m, per] of shade_index)
 		for (const [tex, i] of per) {
 			const image = image_of(tex);
 			shades[i] = Object.assign(material_fields(m), { image, rgb: image ? [0, 0, 0] : solid_color(tex, 'entity texture') });
 		}
-	const sky_image = image_of(sky_texture);
-	const def_sub = sub_of(default_substance);
 	const ns = shades.length;
-	const shade_response = new Int32Array(ns), shade_light = new Int32Array(ns), shade_mirror = new Int32Array(ns);
-	const shade_roughness = new Float64Array(ns), shade_rgb = new Float64Array(3 * ns), shade_image = new Int32Array(ns);
-	shades.forEach((s, i) => {
-		shade_response[i] = s.response; shade_light[i] = s.light; shade_mirror[i] = s.mirror;
-		shade_image[i] = s.image;
-		shade_roughness[i] = s.roughness;
-		shade_rgb[3 * i] = s.rgb[0]; shade_rgb[3 * i + 1] = s.rgb[1]; shade_rgb[3 * i + 2] = s.rgb[2];
-	});
-	const substance_ri = new Float64Array(substances.map((s) => s.refractive_index));
-	return {
-		node_pos, node_size, node_parent, node_child, node_ent_begin, node_ent_count,
-		list_entity: new Int32Array(list), ent_type, ent_geom, ent_shade, ent_substance,
-		shade_response, shade_light, shade_mirror, shade_roughness, shade_rgb, shade_image, substance_ri,
-		images: images.map((t) => ({ width: t.width, height: t.height, rgb: image_bytes(t) })),
-		entities, substances, default_substance_index: def_sub, sky_image,
-		_maps: { ent_index, sub_index, shades, shade_index, images, image_index }
+	const t = {
+		shade_response: new Int32Array(ns), shade_light: new Int32Array(ns), shade_mirror: new Int32Array(ns),
+		shade_roughness: new Float64Array(ns), shade_rgb: new Float64Array(3 * ns), shade_image: new Int32Array(ns)
 	};
+	shades.forEach((s, i) => {
+		t.shade_response[i] = s.response; t.shade_light[i] = s.light; t.shade_mirror[i] = s.mirror;
+		t.shade_image[i] = s.image;
+		t.shade_roughness[i] = s.roughness;
+		t.shade_rgb[3 * i] = s.rgb[0]; t.shade_rgb[3 * i + 1] = s.rgb[1]; t.shade_rgb[3 * i + 2] = s.rgb[2];
+	});
+	return t;
 }
+
+/* ---- O(edit) scene updates: a journal over the reference's own mutators ---------------------------- */
+// The reference edits a scene through a handful of methods: Entity.set_octree (EntitySet delete /
+// add, src/entity.ts:50-56; add_entity_to_octree calls it, src/octree_entity.ts:174-188), Octree.set
+// (new nodes, src/octree.ts:56-70; add_entity_to_octree's tree extension) and the entity setters
+// (_set_pos, set_material, set_texture: src/entities/entity_basic.ts:38-57; set_substance:
+// src/entity.ts:67-71; set_diameter: entity_sphere.ts:45-60; set_size: entity_box.ts:37).  Each is
+// wrapped once, on the prototype that defines it (the reference's code is not changed, and no
+// per-object state is added to entities); the wrapper notes the object in every live Raytracer's
+// journal before the original runs.  invalidate_scene() then sends only the noted nodes and the sets
+// holding noted entities (rt_apply_edit), not the whole scene.
+const JOURNALS = new Set();
+const WRAPPED = Symbol('rt_journal_wrapped');
+const ENTITY_MUTATORS = ['_set_pos', 'set_material', 'set_texture', 'set_substance', 'set_diameter', 'set_size'];
+
+function entity_node(e) { return e._octree !== undefined ? e._octree : e.octree; }
+
+function wrap_method(obj, name, note) {
+	let p = Object.getPrototypeOf(obj);
+	while (p && p !== Object.prototype && !Object.prototype.hasOwnProperty.call(p, name)) p = Object.getPrototypeOf(p);
+	if (!p || p === Object.prototype || typeof p[name] !== 'function' || p[name][WRAPPED]) return;
+	const orig = p[name];
+	const w = function () {
+		if (JOURNALS.size) for (const j of JOURNALS) note(j, this, arguments);
+		return orig.apply(this, arguments);
+	};
+	w[WRAPPED] = true;
+	Object.defineProperty(p, name, { value: w, writable: true, configurable: true, enumerable: false });
+}
+
+function journal_classes(node, entity) {
+	if (node) wrap_method(node, 'set', (j, t) => j.struct.add(t));
+	if (entity) {
+		wrap_method(entity, 'set_octree', (j, e, args) => {
+			const old = entity_node(e);
+			if (old) j.nodes.add(old);
+			if (args[0]) j.nodes.add(args[0]);
+		});
+		for (const m of ENTITY_MUTATORS) wrap_method(entity, m, (j, e) => j.ents.add(e));
+	}
+}
+
+function grow_i32(a, n, fill) {
+	if (a.length >= n) return a;
+	const b = new Int32Array(Math.max(n, 2 * a.length));
+	if (fill !== undefined) b.fill(fill);
+	b.set(a);
+	return b;
+}
+
+// index_within_parent (src/octree_space.ts:113-125), as rt_upload_scene computes it: RT_OCT_BAD (1000)
+// when the geometric index is not 0..7
+function octant_in_parent(t) {
+	const p = t.parent, c = vec(t.id.pos), q = vec(p.id.pos), sc = 2 / p.id.size;
+	const idx = (((c[2] - q[2]) * sc) << 2) + (((c[1] - q[1]) * sc) << 1) + (((c[0] - q[0]) * sc) << 0);
+	return idx >= 0 && idx <= 7 ? idx : 1000;
+}
+
+/**
+ * The edit since the last sync as an rt_edit_desc (include/rt.h) in resident slots, from journal j
+ * and the slot state st (built at the last full sync), or null when the edit cannot be expressed
+ * (a child replaced or removed, a node re-parented, a new ImageTexture, an entity whose node is
+ * unknown): the caller then re-reads the whole scene.  New nodes take the next slots in DFS
+ * pre-order of their subtrees; their DFS ids come from subtree sizes along their paths (O(depth)),
+ * the existing nodes' ids shift on the device.  Updates st and scene._maps in place.
+ */
+function build_edit(scene, st, j, default_substance, sky_texture) {
+	const sym = st.sym, maps = scene._maps;
+	const slot = (t) => t[sym];
+	// 1. structure: new subtrees under existing nodes
+	const new_nodes = [], rec = new Set(), base = st.n_slots;
+	for (const t of j.struct) {
+		const sl = slot(t);
+		if (sl === undefined || sl >= base) continue;    // a node outside the scene, or a new one (below)
+		for (let c = 0; c < 8; c++) {
+			const ch = t.get(c), old = st.child[8 * sl + c];
+			if (ch == undefined) { if (old >= 0) return null; continue; }
+			const cs = slot(ch);
+			if (cs !== undefined) { if (cs !== old) return null; continue; }
+			if (old >= 0 || ch.parent !== t) return null;
+			const stack = [ch];
+			while (stack.length) {
+				const x = stack.pop();
+				if (slot(x) !== undefined) return null;
+				x[sym] = st.n_slots;
+				st.nodes[st.n_slots++] = x;
+				new_nodes.push(x);
+				for (let k = 7; k >= 0; k--) {
+					const y = x.get(k);
+					if (y != undefined) { if (y.parent !== x) return null; stack.push(y); }
+				}
+			}
+			rec.add(sl);
+		}
+	}
+	st.child = grow_i32(st.child, 8 * st.n_slots, -1);
+	st.sub = grow_i32(st.sub, st.n_slots);
+	for (const x of new_nodes) {
+		const sx = slot(x);
+		for (let c = 0; c < 8; c++) {
+			const y = x.get(c);
+			st.child[8 * sx + c] = y != undefined ? slot(y) : -1;
+		}
+		rec.add(sx);
+	}
+	for (const t of rec) {                              // parents that gained a child
+		const x = st.nodes[t];
+		for (let c = 0; c < 8; c++) {
+			const y = x.get(c);
+			st.child[8 * t + c] = y != undefined ? slot(y) : -1;
+		}
+	}
+	// DFS ids of the new nodes: subtree sizes first (every new node counts on its whole path)
+	for (const x of new_nodes) {
+		st.sub[slot(x)] = 0;
+	}
+	for (const x of new_nodes)
+		for (let y = x; y != undefined; y = y.parent) st.sub[slot(y)] += 1;
+	const dfs_new_slot = new Int32Array(new_nodes.length), dfs_new_val = new Int32Array(new_nodes.length);
+	new_nodes.forEach((x, i) => {
+		let id = 0;
+		for (let y = x; y.parent != undefined; y = y.parent) {
+			const p = y.parent;
+			id += 1;
+			for (let c = 0; c < 8; c++) {
+				const z = p.get(c);
+				if (z === y) break;
+				if (z != undefined) id += st.sub[slot(z)];
+			}
+		}
+		dfs_new_slot[i] = slot(x);
+		dfs_new_val[i] = id;
+	});
+	const F = Array.from(dfs_new_val).sort((a, b) => a - b);
+	const dfs_shift = Int32Array.from(F, (f, k) => f - k);
+	// 2. node records, ascending slots
+	const rec_slot = Int32Array.from(Array.from(rec).sort((a, b) => a - b));
+	const nr = rec_slot.length;
+	const rec_cube = new Float64Array(4 * nr), rec_child = new Int32Array(8 * nr), rec_up = new Int32Array(2 * nr);
+	for (let k = 0; k < nr; k++) {
+		const sl = rec_slot[k], x = st.nodes[sl], p = vec(x.id.pos);
+		rec_cube[4 * k] = p[0]; rec_cube[4 * k + 1] = p[1]; rec_cube[4 * k + 2] = p[2]; rec_cube[4 * k + 3] = x.id.size;
+		for (let c = 0; c < 8; c++) rec_child[8 * k + c] = st.child[8 * sl + c];
+		const root = sl === 0;
+		rec_up[2 * k] = root ? -1 : slot(x.parent);
+		rec_up[2 * k + 1] = root ? -1 : octant_in_parent(x);
+	}
+	// 3. dirty EntitySets: noted nodes, the nodes of noted entities, every new node
+	const dirty = new Set(new_nodes.map(slot));
+	for (const t of j.nodes) { const sl = slot(t); if (sl !== undefined) dirty.add(sl); }
+	for (const e of j.ents) {
+		const t = entity_node(e);
+		if (t == undefined) { if (maps.ent_index.has(e)) return null; continue; }
+		const sl = slot(t);
+		if (sl !== undefined) dirty.add(sl);
+	}
+	const set_slot = Int32Array.from(Array.from(dirty).sort((a, b) => a - b));
+	const members = [];
+	const set_begin = new Int32Array(set_slot.length), set_count = new Int32Array(set_slot.length);
+	const new_ents = [];
+	for (let k = 0; k < set_slot.length; k++) {
+		const t = st.nodes[set_slot[k]];
+		set_begin[k] = members.length;
+		const set = t.value ? t.value.set : undefined;
+		if (set) for (const e of set) {
+			if (!maps.ent_index.has(e)) { maps.ent_index.set(e, scene.entities.length); scene.entities.push(e); new_ents.push(e); }
+			members.push(e);
+		}
+		set_count[k] = members.length - set_begin[k];
+	}
+	const nm = members.length;
+	const set_ent = new Int32Array(nm), set_type = new Int32Array(nm), set_shade = new Int32Array(nm);
+	const set_geom = new Float64Array(9 * nm);
+	members.forEach((e, i) => {
+		set_ent[i] = maps.ent_index.get(e);
+		set_type[i] = entity_geom(e, set_geom.subarray(9 * i, 9 * i + 9));
+		set_shade[i] = shade_row(maps.shade_index, maps.shades, e);
+	});
+	// 4. substances of the noted and the new entities
+	const subs = new Set();
+	for (const e of j.ents) if (maps.ent_index.has(e)) subs.add(maps.ent_index.get(e));
+	for (const e of new_ents) subs.add(maps.ent_index.get(e));
+	const sub_ent = Int32Array.from(Array.from(subs).sort((a, b) => a - b));
+	const sub_val = Int32Array.from(sub_ent, (i) => maps.sub_of(scene.entities[i].get_substance()));
+	// 5. tables: every shade row re-read; a new ImageTexture needs the image table (full upload)
+	const no_new_image = (tex) => {
+		if (!loaded_image(tex)) return 0;
+		if (!maps.image_index.has(tex)) throw NEW_IMAGE;
+		return maps.image_index.get(tex);
+	};
+	let tables;
+	try {
+		tables = shade_tables(maps.shades, maps.shade_index, no_new_image);
+		no_new_image(sky_texture);
+	} catch (err) {
+		if (err !== NEW_IMAGE) throw err;
+		return null;                                     // (rows added above are filled by the full path)
+	}
+	maps.sub_of(default_substance);
+	// rough mirrors listed (rt_create's scatter gate): a row in use by a member of any set
+	st.ent_shade = grow_i32(st.ent_shade, scene.entities.length, -1);
+	for (let i = 0; i < nm; i++) st.ent_shade[set_ent[i]] = set_shade[i];
+	let scatter = 0;
+	const rough = maps.shades.map((r) => !r.light && r.response === 0 && r.mirror && r.roughness > 0);
+	if (rough.some((x) => x))
+		for (let i = 0; i < scene.entities.length && !scatter; i++)
+			if (st.ent_shade[i] >= 0 && rough[st.ent_shade[i]] && entity_node(scene.entities[i]) != undefined) scatter = 1;
+	return Object.assign({
+		n_slots: st.n_slots, n_entities: scene.entities.length,
+		rec_slot, rec_cube, rec_child, rec_up, set_slot, set_begin, set_count, set_ent, set_type, set_shade, set_geom,
+		sub_ent, sub_val, dfs_new_slot, dfs_new_val, dfs_shift, scatter,
+		substance_ri: new Float64Array(scene.substances.map((x) => x.refractive_index))
+	}, tables);
+}
+const NEW_IMAGE = { rt_new_image: true };
 
 /* ---- camera / config ---------------------------------------------------------------------------- */
 
@@ -271,6 +503,10 @@ class Raytracer {
 		this.options = Object.assign({ device: 0 }, options || {});
 		this._ctx = null;
 		this._scene = null;
+		this._journal = null;           // edits noted since the last sync (JOURNALS)
+		this._st = null;                // resident slots of the scene's nodes (build_edit)
+		this._sym = Symbol('rt_slot');  // this Raytracer's slot property on the octree's nodes
+		this._full = false;
 		this.last_stats = null;
 		this.last_hit_entity = null;
 		this.last_hit_node = null;
@@ -282,14 +518,60 @@ class Raytracer {
 	get tree() { return this.otree; }
 	get rng() { return this._rng; }
 
-	/** Re-flatten the octree before the next frame (call after adding / moving entities or changing
-	 * materials).  The GPU copy is then updated incrementally (rt_update_scene): only the nodes
-	 * whose EntitySet or member entities changed are rebuilt and sent; `last_update` reports it. */
-	invalidate_scene() { this._dirty = true; }
+	/** Bring the GPU copy of the scene up to date before the next frame (call after adding / moving
+	 * entities or changing materials).  Edits made through the reference's own mutators
+	 * (add_entity_to_octree, Entity.set_octree / _set_pos / set_material / set_texture /
+	 * set_substance / set_diameter / set_size, Octree.set) are journaled as they happen, and only
+	 * the nodes and EntitySets they touched are read and sent (rt_apply_edit, O(edit)).
+	 * `invalidate_scene({ full: true })` re-reads the whole octree instead (after direct field writes
+	 * that bypass those methods); the GPU copy is then diffed and patched (rt_update_scene).
+	 * `last_update` reports what was sent. */
+	invalidate_scene(opts) {
+		this._dirty = true;
+		if (opts && opts.full) this._full = true;
+	}
 
 	/** Release the GPU context now instead of at garbage collection. */
 	close() {
+		if (this._journal) { JOURNALS.delete(this._journal); this._journal = null; }
+		this._st = null;
 		if (this._ctx) { load_addon().destroy(this._ctx); this._ctx = null; }
+	}
+
+	// After a full read of the scene: the resident slot of every node (slots: sceneSlots' map; null =
+	// DFS order), subtree sizes, child slots, and a fresh journal.
+	_begin_journal(slots, n_slots) {
+		const sc = this._scene, n = sc.node_size.length, sym = this._sym;
+		if (this._st) for (const x of this._st.nodes) if (x) delete x[sym];
+		const slot = (k) => (slots ? slots[k] : k);
+		const st = { sym, n_slots, nodes: new Array(n_slots).fill(null), child: new Int32Array(8 * n_slots).fill(-1),
+			sub: new Int32Array(n_slots), ent_shade: Int32Array.from(sc.ent_shade) };
+		for (let k = 0; k < n; k++) {
+			const x = sc._nodes[k], sl = slot(k);
+			x[sym] = sl;
+			st.nodes[sl] = x;
+			for (let c = 0; c < 8; c++) {
+				const ch = sc.node_child[8 * k + c];
+				st.child[8 * sl + c] = ch >= 0 ? slot(ch) : -1;
+			}
+		}
+		for (let k = n - 1; k >= 0; k--) {             // DFS pre-order: children after their parent
+			st.sub[slot(k)] += 1;
+			if (k > 0) st.sub[slot(sc.node_parent[k])] += st.sub[slot(k)];
+		}
+		this._st = st;
+		if (!this._journal) {
+			this._journal = { nodes: new Set(), ents: new Set(), struct: new Set() };
+			JOURNALS.add(this._journal);
+		}
+		const j = this._journal;
+		j.nodes.clear(); j.ents.clear(); j.struct.clear();
+		const seen = new Set();
+		journal_classes(this.otree, null);
+		for (const e of sc.entities) {
+			const p = Object.getPrototypeOf(e);
+			if (!seen.has(p)) { seen.add(p); journal_classes(null, e); }
+		}
 	}
 
 	_sync_scene() {
@@ -304,9 +586,32 @@ class Raytracer {
 		if (!this._scene) {
 			this._scene = serialize_scene(this.otree, this.config.default_substance, undefined, sky);
 			a.uploadScene(this._ctx, this._scene);
+			const sl = a.sceneSlots(this._ctx, this._scene.node_size.length);
+			this._begin_journal(sl.slots, sl.n_slots);
 		} else if (this._dirty) {
-			this._scene = serialize_scene(this.otree, this.config.default_substance, this._scene, sky);
-			this.last_update = a.updateScene(this._ctx, this._scene);
+			let u = null;
+			if (!this._full && this._st) {
+				const t0 = process.hrtime();
+				const edit = build_edit(this._scene, this._st, this._journal, this.config.default_substance, sky);
+				if (edit) u = a.applyEdit(this._ctx, edit);     // null: the store asks for a full upload
+				if (u) {
+					const dt = process.hrtime(t0);
+					u.js_ms = dt[0] * 1e3 + dt[1] / 1e6;          // journal -> edit -> applied, host side
+					u.via = 'edit';
+					const j = this._journal;
+					j.nodes.clear(); j.ents.clear(); j.struct.clear();
+				}
+			}
+			if (!u) {
+				this._scene = serialize_scene(this.otree, this.config.default_substance, this._scene, sky);
+				u = a.updateScene(this._ctx, this._scene);
+				u.via = 'scene';
+				const sl = a.sceneSlots(this._ctx, this._scene.node_size.length);
+				if (sl) this._begin_journal(sl.slots, sl.n_slots);
+				else this._st = null;
+			}
+			this._full = false;
+			this.last_update = u;
 		}
 		this._dirty = false;
 		return this._scene;
@@ -430,5 +735,6 @@ class FaceEntity {
 
 module.exports = {
 	Raytracer, FaceEntity, serialize_scene, camera_desc, load_addon,
-	RT_ENT_SPHERE, RT_ENT_BOX, RT_ENT_FACE
+	RT_ENT_SPHERE, RT_ENT_BOX, RT_ENT_FACE,
+	_internal: { build_edit }                 // tests/js/check_edit.js
 };

@@ -177,7 +177,7 @@ def declare(lib):
     lib.rt_tonemap_range.argtypes = [_i, P(rt_exposure_stats), _i, _d, _d, _pd]
     lib.rt_update_scene.argtypes = [vp, P(rt_scene_desc), P(rt_update_stats)]
     lib.rt_apply_edit.argtypes = [vp, P(rt_edit_desc), P(rt_update_stats)]
-    lib.rt_scene_node_slots.argtypes = [vp, _pi, _i]
+    lib.rt_scene_node_slots.argtypes = [vp, _pi, _i, _pi]
     lib.rt_builder_sync.argtypes = [vp, vp, P(rt_shade), _i, _pd, _i, P(rt_update_stats)]
     lib.rt_builder_move.argtypes = [vp, _i, _pd]
     lib.rt_builder_set_shade.argtypes = [vp, _i, _i, _i]

@@ -4,11 +4,12 @@
  * Builds reference-shaped objects, checks serialize_scene() reproduces the linearised arrays, and
  * (unless --serialize-only) renders one frame with the drop-in Raytracer into ExposureBuffer.pixels.
  * --scatter: rough mirrors with options.scatter = 'counter', the rng's one draw = seed / 2^53.
- * --edit A B C: after the first frame, edit the live scene the way a host program does and render
- *   again into <out_prefix>.2.* (the resident scene is updated incrementally, rt_update_scene):
- *   sphere A is moved to (0.5, 0.5, 0.8) (Entity._set_pos + Set.delete / Set.add into the root's
- *   EntitySet, which is where add_entity_to_octree files a cube straddling the centre planes), and
- *   entity B takes entity C's material and texture (set_material / set_texture).
+ * --edit A B C x y z depth [--direct]: after the first frame, edit the live scene the way a host
+ *   program does and render again into <out_prefix>.2.*: sphere A moves to (x, y, z) (_set_pos, then
+ *   add_entity_to_octree with max_in_depth = depth, which may create nodes), and entity B takes
+ *   entity C's material and texture (set_material / set_texture).  The drop-in journals these calls
+ *   and sends only what they touched (rt_apply_edit).  --direct makes the same edit by writing the
+ *   fields and Sets directly and calls invalidate_scene({ full: true }) (a full re-read, rt_update_scene).
  * --devices: options.devices (one context over several GPUs, or several parts on one GPU).
  * --plain: options {} (no ids, no counters), the default path a host takes; only pixels are written.
  * --repeat N: after the first frame, N frames timed each with options.stats off, then N with it on
@@ -109,19 +110,32 @@ if (ri > 0) {
 
 const ei = process.argv.indexOf('--edit');
 if (ei > 0) {
-	const [A, B, C] = process.argv.slice(ei + 1, ei + 4).map(Number);
+	const [A, B, C, px, py, pz, depth] = process.argv.slice(ei + 1, ei + 8).map(Number);
+	const direct = process.argv.includes('--direct');
 	const ea = world.entities[A], eb2 = world.entities[B], ec = world.entities[C];
-	const home = world.nodes.find((t) => t.value.set.has(ea));
-	home.value.set.delete(ea);                                   // Entity.set_octree: Set.delete ...
-	const p = [0.5, 0.5, 0.8];
-	ea.pos = { v: p };                                           // SphereEntity._set_pos
-	ea.sphere_math._pos = ea.pos;                                //  -> Sphere.update_cache
-	ea.sphere_math._dot_pp = ((0 + p[0] * p[0]) + p[1] * p[1]) + p[2] * p[2];
-	ea.sphere_math._radius_sq = ea.sphere_math._radius * ea.sphere_math._radius;
-	world.root.value.set.add(ea);                                // ... Set.add (to the end)
-	eb2.material = ec.material;                                  // set_material
-	eb2.texture = ec.texture;                                    // set_texture
-	tracer.invalidate_scene();
+	const p = [px, py, pz];
+	if (!direct) {
+		// through the reference's mutators (journaled): move_entity's steps, then the material swap
+		ea._set_pos({ v: p });
+		rs.add_entity_to_octree(world.root, ea, { max_in_depth: depth, max_out_depth: 0 });
+		eb2.set_material(ec.get_material());
+		eb2.set_texture(ec.get_texture());
+		tracer.invalidate_scene();
+	} else {
+		// direct field writes that bypass the mutators: only a full re-read sees them
+		const home = ea._octree;
+		home.value.set.delete(ea);
+		ea.pos = { v: p };
+		ea.sphere_math._pos = ea.pos;
+		ea.sphere_math._dot_pp = ((0 + p[0] * p[0]) + p[1] * p[1]) + p[2] * p[2];
+		const t = rs.add_entity_to_octree(world.root, { get_aabb: () => ea.get_aabb(), set_octree() {} },
+			{ max_in_depth: depth, max_out_depth: 0 });                // where it belongs (nodes made with Octree.set)
+		t.value.set.add(ea);
+		ea._octree = t;
+		eb2.material = ec.material;
+		eb2.texture = ec.texture;
+		tracer.invalidate_scene({ full: true });
+	}
 	tracer.trace_frame();
 	write_frame(out_prefix + '.2', { update: tracer.last_update });
 }

@@ -535,3 +535,18 @@ def test_post_light_reseat_throws_like_the_reference(ctx, textured):
     st = ctx.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True)
     _same_frames(got, st)
     assert st["stats"].counters() == full["counters"]
+
+
+@pytest.mark.parametrize("top", ["1", "2", "3"])
+def test_top_levels_layout_equals_oracle(top, monkeypatch):
+    """RT_TOP_LEVELS: the nodes of depth <= top take slots 0.. breadth-first; frames,
+    node ids (through node_dfs) and walker stop sequences are unchanged."""
+    monkeypatch.setenv("RT_TOP_LEVELS", top)
+    c = rtamd.Context(0)
+    try:
+        for spec, wh, refmax in ((scenes.small_random(2), (160, 120), 3), (scenes.config1_spheres(), (128, 96), 4)):
+            ref, got = _run_both(c, spec, scenes.make_camera(*wh), scenes.make_config(refmax))
+            _compare(ref, got)
+            assert got["stats"].counters() == ref["counters"]
+    finally:
+        c.close()

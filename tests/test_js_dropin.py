@@ -56,6 +56,33 @@ def test_serialize_matches_native_builder(tmp_path, name):
     assert "serialize ok" in out
 
 
+EDIT_OPS = {
+    "move_root": ("config1", [{"op": "move", "entity": 0, "pos": [0.5, 0.5, 0.8], "depth": 3}]),
+    "move_new_nodes": ("small4", [{"op": "move", "entity": 9,
+                                    "pos": [0.22770041975507802, 0.5219043192384103, 0.2345159569779426], "depth": 5}]),
+    "many": ("small4", [{"op": "move", "entity": 9, "pos": [0.22770041975507802, 0.5219043192384103, 0.2345159569779426], "depth": 5},
+                        {"op": "move", "entity": 13, "pos": [0.8287902268064543, 0.2703745559931393, 0.7072929461731522], "depth": 5},
+                        {"op": "add_sphere", "pos": [0.7044694202017586, 0.29964738052273826, 0.18759090183548752], "d": 0.04, "depth": 6, "like": 5},
+                        {"op": "add_sphere", "pos": [0.31, 0.62, 0.9], "d": 0.01, "depth": 7, "like": 2},
+                        {"op": "shade", "entity": 3, "like": 1}, {"op": "substance", "entity": 7, "like": 1},
+                        {"op": "move", "entity": 5, "pos": [0.5, 0.5, 0.5], "depth": 5}]),
+    "config2_moves": ("config2", [{"op": "shade", "entity": 10, "like": 20}]),
+}
+
+
+@pytest.mark.parametrize("name", sorted(EDIT_OPS))
+def test_edit_journal_equals_fresh_linearisation(tmp_path, name):
+    """CPU: the rt_edit_desc that the drop-in's journal builds, applied to the first linearisation as
+    rt_apply_edit applies it (records, sets, substances, DFS ids and shift), equals a fresh
+    serialize_scene of the edited tree (tests/js/check_edit.js)."""
+    scene, ops = EDIT_OPS[name]
+    spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4), "config2": scenes.config2}[scene]()
+    path = _dump(tmp_path, spec, scenes.make_camera(8, 8), scenes.make_config(2))
+    (tmp_path / "ops.json").write_text(json.dumps(ops))
+    out = _node([os.path.join(ROOT, "tests", "js", "check_edit.js"), path, str(tmp_path / "ops.json")])
+    assert "edit ok" in out, out
+
+
 def test_addon_loads_and_fails_loudly_without_gpu():
     """The addon loads; with no GPU create() throws RT_E_NODEVICE (never a silent CPU path)."""
     js = ("const rt=require(%r);const a=rt.load_addon();"
@@ -139,19 +166,35 @@ def test_dropin_default_options_frame_equals_oracle(tmp_path, name, wh, band_min
     assert "frame_ms" in st and "segments" not in st, st          # no counters: the split passes ran
 
 
+EDITS = {
+    # scene, moved sphere A, entity B takes C's material, A's new position; the second one creates
+    # three octree nodes (add_entity_to_octree extends the tree inward)
+    "root": (scenes.config1_spheres, 0, 3, 1, (0.5, 0.5, 0.8)),
+    "new_nodes": (lambda: scenes.small_random(4), 9, 3, 1, (0.22770041975507802, 0.5219043192384103, 0.2345159569779426)),
+}
+
+
 @pytest.mark.gpu
-def test_dropin_scene_edit_updates_incrementally(tmp_path):
-    """invalidate_scene() after editing the live scene: the second frame comes from rt_update_scene
-    (stable ids from serialize_scene(prev)) and equals the oracle after the same edits."""
-    spec = scenes.config1_spheres()
+@pytest.mark.parametrize("mode", ["journal", "direct"])
+@pytest.mark.parametrize("edit", sorted(EDITS))
+def test_dropin_scene_edit_updates_incrementally(tmp_path, edit, mode):
+    """Edits of the live scene after a first frame.  journal: through the reference's mutators
+    (_set_pos + add_entity_to_octree, set_material / set_texture), which the drop-in journals and
+    sends as one rt_apply_edit (O(edit): only the touched nodes and sets); direct: the same edit by
+    field writes, then invalidate_scene({full: true}) (a full re-read diffed by rt_update_scene).  The
+    second frame equals the oracle after the same edits."""
+    factory, A, B, Cc, pos = EDITS[edit]
+    spec = factory()
     cam, cfg = scenes.make_camera(160, 120), scenes.make_config(3)
     path = _dump(tmp_path, spec, cam, cfg)
-    A, B, Cc = 0, 3, 1                      # move sphere 0; entity 3 takes entity 1's (mirror) material
-    _node([RUNNER, path, str(tmp_path / "out"), "--edit", str(A), str(B), str(Cc)])
-    w, root = oracle.build_scene(spec)
     e = spec.entities
-    w.move_entity(root, A, (0.5, 0.5, 0.8), e[A]["max_in_depth"], e[A]["max_out_depth"])
+    args = [str(A), str(B), str(Cc)] + [repr(float(x)) for x in pos] + [str(int(e[A]["max_in_depth"]))]
+    _node([RUNNER, path, str(tmp_path / "out"), "--edit"] + args + (["--direct"] if mode == "direct" else []))
+    w, root = oracle.build_scene(spec)
+    n0 = len(w.linearize(root)["node_size"])
+    w.move_entity(root, A, pos, e[A]["max_in_depth"], e[A]["max_out_depth"])
     w.set_shade(B, e[Cc]["shade"], e[B]["substance"])
+    n1 = len(w.linearize(root)["node_size"])
     ref = w.trace_frame(root, cam, cfg, nthreads=8)
     o = str(tmp_path / "out.2")
     rgb = np.fromfile(o + ".rgb", dtype=np.float32)
@@ -160,6 +203,11 @@ def test_dropin_scene_edit_updates_incrementally(tmp_path):
     assert np.array_equal(np.fromfile(o + ".node", dtype=np.int32), ref["hit_node"])
     assert np.array_equal(np.fromfile(o + ".status", dtype=np.uint8), ref["status"])
     upd = json.loads((tmp_path / "out.2.json").read_text())["update"]
-    assert upd["full"] == 0 and 1 <= upd["dirty_nodes"] <= 4, upd
+    assert upd["full"] == 0, upd
+    assert upd["via"] == ("edit" if mode == "journal" else "scene"), upd
+    assert upd["new_nodes"] == n1 - n0, (upd, n0, n1)
+    if mode == "journal":
+        # the moved sphere's old and new node, B's node, and the new nodes
+        assert 1 <= upd["dirty_nodes"] <= 3 + (n1 - n0), upd
     first = np.fromfile(tmp_path / "out.rgb", dtype=np.float32)
     assert not np.array_equal(first, rgb)

@@ -141,8 +141,11 @@ def _same(a, b, keys=("rgb", "hit_entity", "hit_node", "status")):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [1, 4])
-def test_update_equals_full_upload_and_oracle(seed):
+@pytest.mark.parametrize("seed,top", [(1, None), (4, None), (4, "3")])
+def test_update_equals_full_upload_and_oracle(seed, top, monkeypatch):
+    """top: RT_TOP_LEVELS (the upper levels take the first slots, breadth-first)."""
+    if top:
+        monkeypatch.setenv("RT_TOP_LEVELS", top)
     spec = scenes.small_random(seed, n_tri=600)
     cam, cfg = scenes.make_camera(160, 120), scenes.make_config(3)
     p = Pair(spec)
@@ -241,11 +244,14 @@ def test_update_shade_table_and_scatter_gate():
 
 # ---- rt_builder_sync: O(edit) re-upload from the builder's journal ---------------------------------------------
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", [1, 4])
-def test_builder_sync_equals_full_upload_and_oracle(seed):
+@pytest.mark.parametrize("seed,top", [(1, None), (4, None), (1, "2")])
+def test_builder_sync_equals_full_upload_and_oracle(seed, top, monkeypatch):
     """rt_builder_sync after each edit of the script: only the edit's nodes travel (no linearisation,
     no diff of the whole scene), and the frame equals a fresh rt_upload_scene of the builder's
-    linearised tree and, periodically, the oracle's frame."""
+    linearised tree and, periodically, the oracle's frame.  top: RT_TOP_LEVELS (the full sync's slots
+    are not DFS order; the builder takes them from the store)."""
+    if top:
+        monkeypatch.setenv("RT_TOP_LEVELS", top)
     spec = scenes.small_random(seed, n_tri=600)
     cam, cfg = scenes.make_camera(160, 120), scenes.make_config(3)
     p = Pair(spec)

@@ -1,0 +1,6 @@
+set -u
+OUT=gpurun_out/r3v5
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1 || exit $?
+timeout -k 10 300 node tools/js_edit_time.js 1000000 256 > $OUT/js_edit_time.log 2>&1 || exit $?
