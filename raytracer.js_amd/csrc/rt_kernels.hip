@@ -60,6 +60,38 @@ enum : uint32_t { NODE_CHILD = 32, NODE_BOX = 64, NODE_NENT = 96, NODE_UP = 112 
 extern __shared__ RtNode s_top[];
 #endif
 
+// RT_BUF_LOADS: node records through raw buffer loads (a V# over the node array in SGPRs, the 32-bit
+// record offset in one VGPR, the field in the instruction's offset): no 64-bit address arithmetic.
+#ifndef RT_BUF_LOADS
+#define RT_BUF_LOADS 0
+#endif
+#if RT_BUF_LOADS
+typedef unsigned int rt_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int rt_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const RtDevScene &S)
+{
+    // raw buffer (stride 0), the whole 4 GB offset range, gfx9 dword3 (as ck_tile's gfx9 resources)
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<RtNode *>(S.node), (short)0, (int)0xffffffff, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ T buf_ld(const RtDevScene &S, uint32_t voff, uint32_t field)
+{
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8 || sizeof(T) == 16, "buffer load size");
+    T v;
+    if constexpr (sizeof(T) == 4) {
+        const unsigned int x = __builtin_amdgcn_raw_buffer_load_b32(node_rsrc(S), (int)(voff + field), 0, 0);
+        __builtin_memcpy(&v, &x, 4);
+    } else if constexpr (sizeof(T) == 8) {
+        const rt_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(node_rsrc(S), (int)(voff + field), 0, 0);
+        __builtin_memcpy(&v, &x, 8);
+    } else {
+        const rt_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(node_rsrc(S), (int)(voff + field), 0, 0);
+        __builtin_memcpy(&v, &x, 16);
+    }
+    return v;
+}
+#endif
+
 template <typename T>
 __device__ __forceinline__ T ld_node(const RtDevScene &S, int n, uint32_t field)
 {
@@ -67,7 +99,20 @@ __device__ __forceinline__ T ld_node(const RtDevScene &S, int n, uint32_t field)
     if ((unsigned)n < (unsigned)S.n_lds)
         return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(s_top) + node_off(n) + field);
 #endif
+#if RT_BUF_LOADS
+    if constexpr (sizeof(T) == 32) {          // the cube: two 16-byte loads
+        T v;
+        const rt_u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(node_rsrc(S), (int)(node_off(n) + field), 0, 0);
+        const rt_u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(node_rsrc(S), (int)(node_off(n) + field + 16), 0, 0);
+        __builtin_memcpy(&v, &a, 16);
+        __builtin_memcpy(reinterpret_cast<char *>(&v) + 16, &b, 16);
+        return v;
+    } else {
+        return buf_ld<T>(S, node_off(n), field);
+    }
+#else
     return ld_at<T>(S.node, node_off(n) + field);
+#endif
 }
 
 // a walk kernel's prologue: the workgroup's copy of slots [0, S.n_lds)
@@ -93,7 +138,8 @@ __device__ __forceinline__ NodeDims node_dims(const RtDevScene &S, int n)
 
 __device__ __forceinline__ int node_child(const RtDevScene &S, int n, int oct)
 {
-    return ld_node<int32_t>(S, n, NODE_CHILD + ((uint32_t)oct << 2));
+    // (oct & 7): callers pass 0..7; the mask lets the compiler fold the field into the record offset
+    return ld_node<int32_t>(S, n, NODE_CHILD + (((uint32_t)oct & 7u) << 2));
 }
 
 // {up_tree, up_oct, up2_tree, up2_oct} of node n (one 16-byte load)
@@ -504,13 +550,20 @@ enum : int { A_NONE = 0, A_STEPIN = 1, A_EXIT = 2, A_MOVE = 3 };
 #define RT_PEEK 1
 #endif
 
+#ifndef RT_HEAD_LEAN
+#define RT_HEAD_LEAN 1
+#endif
 template <bool STOP, typename Emit>
 __device__ __forceinline__ void trip_head(const RtDevScene &S, Walker &w, Emit &&emit, int stop, int &res, int &act,
                                           int &lnode, int4 &up)
 {
     act = A_NONE;
+#if !RT_HEAD_LEAN
     lnode = -1;
     up = make_int4(-1, RT_OCT_UNDEF, -1, RT_OCT_UNDEF);
+#endif
+    // (RT_HEAD_LEAN: lnode / up are read by trip_step only for the actions that set them here, so
+    // the early exits below need no defaults, and the compiler no copies of them per exit)
     if (res != 1) return;
     const int ltree = w.cur_tree, loct = w.cur_oct;
     if (++w.steps > STEP_CAP) {
@@ -1867,6 +1920,9 @@ __device__ __forceinline__ bool early_shade(const RtLaunch &L, const RaySrc &src
     return true;
 }
 
+#ifndef RT_FIRST_PIPE
+#define RT_FIRST_PIPE 0
+#endif
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
 {
@@ -1891,6 +1947,26 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
         if (cn >= 4 && !fault) {
             const RayBox rb = make_raybox(src.o, src.d);
             const int n = cn >> 2;
+#if RT_FIRST_PIPE
+            // software pipeline over the list: while candidate k's hierarchy is walked, candidate
+            // k + 1's record header and candidate k + 2's id are already loading
+            int node = cand_load(L.cand, 0, (uint32_t)stride, (uint32_t)src.id);
+            int nxt = n > 1 ? cand_load(L.cand, 1, (uint32_t)stride, (uint32_t)src.id) : 0;
+            int4 ent = ld_node<int4>(S, node, NODE_NENT);        // {n_ent, ent_begin, bvh_root, -}
+            for (int k = 0; k < n; k++) {
+                const int4 ent_n = k + 1 < n ? ld_node<int4>(S, nxt, NODE_NENT) : ent;
+                const int nxt2 = k + 2 < n ? cand_load(L.cand, k + 2, (uint32_t)stride, (uint32_t)src.id) : 0;
+                Hit h;
+                int rank;
+                long long box = 0;
+                const int hk = node_first_hit<false>(S, make_int4(ent.y, ent.x, ent.z, 0), src.o, src.d, rb,
+                                                     L.cull != 0, c, box, h, rank, true);
+                if (hk >= 0) { res = make_int2(node, hk); break; }
+                node = nxt;
+                nxt = nxt2;
+                ent = ent_n;
+            }
+#else
             for (int k = 0; k < n; k++) {
                 const int node = cand_load(L.cand, k, (uint32_t)stride, (uint32_t)src.id);
                 const RtNode &nd = S.node[node];               // the line k_walk read for this candidate
@@ -1901,6 +1977,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
                 const int hk = node_first_hit<false>(S, ent, src.o, src.d, rb, L.cull != 0, c, box, h, rank, true);
                 if (hk >= 0) { res = make_int2(node, hk); break; }
             }
+#endif
         }
         if (RT_EARLY_SHADE && L.level == 0) {
             // level 0: end the plain terminal rays here; queue the rest for k_shade (ray_cn is free at

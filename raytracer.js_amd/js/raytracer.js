@@ -544,8 +544,11 @@ class Raytracer {
 		const sc = this._scene, n = sc.node_size.length, sym = this._sym;
 		if (this._st) for (const x of this._st.nodes) if (x) delete x[sym];
 		const slot = (k) => (slots ? slots[k] : k);
-		const st = { sym, n_slots, nodes: new Array(n_slots).fill(null), child: new Int32Array(8 * n_slots).fill(-1),
-			sub: new Int32Array(n_slots), ent_shade: Int32Array.from(sc.ent_shade) };
+		// mirrors with headroom, so that the edits of many frames never copy them
+		const cap = n_slots + (n_slots >> 3) + 1024, ecap = sc.ent_shade.length + (sc.ent_shade.length >> 3) + 1024;
+		const st = { sym, n_slots, nodes: new Array(n_slots).fill(null), child: new Int32Array(8 * cap).fill(-1),
+			sub: new Int32Array(cap), ent_shade: new Int32Array(ecap).fill(-1) };
+		st.ent_shade.set(sc.ent_shade);
 		for (let k = 0; k < n; k++) {
 			const x = sc._nodes[k], sl = slot(k);
 			x[sym] = sl;
@@ -593,10 +596,12 @@ class Raytracer {
 			if (!this._full && this._st) {
 				const t0 = process.hrtime();
 				const edit = build_edit(this._scene, this._st, this._journal, this.config.default_substance, sky);
+				const t1 = process.hrtime(t0);
 				if (edit) u = a.applyEdit(this._ctx, edit);     // null: the store asks for a full upload
 				if (u) {
 					const dt = process.hrtime(t0);
-					u.js_ms = dt[0] * 1e3 + dt[1] / 1e6;          // journal -> edit -> applied, host side
+					u.build_ms = t1[0] * 1e3 + t1[1] / 1e6;        // journal -> rt_edit_desc (JS)
+					u.js_ms = dt[0] * 1e3 + dt[1] / 1e6;          // ... -> applied (JS + addon + librt)
 					u.via = 'edit';
 					const j = this._journal;
 					j.nodes.clear(); j.ents.clear(); j.struct.clear();

@@ -11,7 +11,7 @@ for CFG in ${CONFIGS:-config3 config5}; do
   for E in $CASES; do
     N=${E%%=*}; R=${E#*=}; P=${R%%:*}; K=${R#*:}
     if [ -n "$P" ]; then export RT_LIB=$PWD/$P; else unset RT_LIB; fi
-    rm -rf "$OUT/$CFG/$N"
+    rm -rf "$OUT/$CFG/$N"; mkdir -p "$OUT/$CFG"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/$CFG/$N" -o kt --output-format csv -- \
         python3 tools/sweep.py --config $CFG --frames $FR "$N:$K" > "$OUT/$CFG/$N.log" 2>&1 || { echo "$CFG $N failed"; tail -5 "$OUT/$CFG/$N.log"; exit 1; }
     python3 - "$OUT/$CFG/$N" $((FR + 3)) "$CFG $N" <<'PY'

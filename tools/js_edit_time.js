@@ -2,9 +2,10 @@
  * js_edit_time.js [n_entities] [width] — cost of scene edits through the JS drop-in on a GPU box.
  * Builds a scene of n random spheres (default 1M) with the test fixture's add_entity_to_octree
  * (max_in_depth 10), renders a first frame (full serialize + upload), then times, for 1 and 100
- * moves: the moves themselves, invalidate_scene() + trace_frame() through the journal (rt_apply_edit),
- * and the same through a full re-read (invalidate_scene({ full: true }), rt_update_scene), each
- * against a plain trace_frame() of the same frame.  One JSON line per case.
+ * moves: the moves themselves, invalidate_scene() + trace_frame() through the journal (rt_apply_edit;
+ * 15 repetitions: median, min, max and the first), and the same through a full re-read
+ * (invalidate_scene({ full: true }), rt_update_scene; 2 repetitions), each against a plain
+ * trace_frame() of the same frame.  One JSON line per case.
  */
 'use strict';
 const rs = require('../tests/js/refshape.js');
@@ -60,7 +61,7 @@ function moves(n) {
 for (const mode of ['journal', 'full']) {
 	for (const n of [1, 100]) {
 		const rows = [];
-		for (let rep = 0; rep < (mode === 'full' ? 2 : 5); rep++) {
+		for (let rep = 0; rep < (mode === 'full' ? 2 : 15); rep++) {
 			const mv = moves(n);
 			const a = process.hrtime();
 			tr.invalidate_scene(mode === 'full' ? { full: true } : undefined);
@@ -68,11 +69,13 @@ for (const mode of ['journal', 'full']) {
 			const tot = ms(a);
 			rows.push({ moves_ms: mv, sync_and_frame_ms: tot, update: tr.last_update });
 		}
+		const first = rows[0].sync_and_frame_ms;
 		rows.sort((x, y) => x.sync_and_frame_ms - y.sync_and_frame_ms);
 		const r = rows[rows.length >> 1];
 		console.log(JSON.stringify({ mode, moves: n, reps: rows.length, moves_ms: +r.moves_ms.toFixed(3),
 			invalidate_plus_frame_ms: +r.sync_and_frame_ms.toFixed(3), edit_cost_ms: +(r.sync_and_frame_ms - plain[2]).toFixed(3),
-			update: r.update }));
+			first_ms: +first.toFixed(3), max_ms: +rows[rows.length - 1].sync_and_frame_ms.toFixed(3),
+			min_ms: +rows[0].sync_and_frame_ms.toFixed(3), update: r.update }));
 	}
 }
 tr.close();
