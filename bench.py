@@ -371,7 +371,8 @@ _PROF_WALL = []          # wall seconds of each completed rocprofv3 pass (report
 def _after_first_frame(rows, key):
     """The rows of a rocprofv3 CSV from the second frame on (the --pmc-child's warm-up frame is the
     first): dispatches at or after the second k_frame_start, ordered by `key`."""
-    starts = sorted(int(r[key]) for r in rows if _kernel_base(r["Kernel_Name"]) == "k_frame_start")
+    # (a counter CSV has one row per counter and dispatch: the dispatches, once each)
+    starts = sorted(set(int(r[key]) for r in rows if _kernel_base(r["Kernel_Name"]) == "k_frame_start"))
     if len(starts) < 2:
         return rows
     return [r for r in rows if int(r[key]) >= starts[1]]

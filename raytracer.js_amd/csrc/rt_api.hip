@@ -131,6 +131,13 @@ struct rt_ctx {
     int bands = 2;                   // RT_BANDS (1: one launch sequence per frame)
     int band_order = 0;              // RT_BAND_ORDER: bit 0 level-0 walks in band order, bit 1 stream
                                      // priorities by band (both measured slower or neutral, §5.14)
+    // Small frames of light scenes run the fused k_trace: one launch instead of ~10.  RT_FUSE_MAX: parts
+    // of at most this many pixels; RT_FUSE_LIST: scenes of at most this many list entries (the fused
+    // loop pays every wave's slowest entity tests at every stop, so heavy scenes keep the split
+    // passes at any size).  Config 1, 256^2: 0.45 -> 0.17 ms; config 3's scene at 128^2: fused 2.2x
+    // slower.
+    int64_t fuse_max = 1 << 18;
+    int64_t fuse_list = 4096;
     int64_t band_min = 1 << 20;      // RT_BAND_MIN: frames of fewer pixels run as one launch (256^2: 0.44 ms
                                      // one launch against 0.61 in 2 bands; 1080p and up gain, §5.14)
     int n_band = 0;                  // band states initialised
@@ -220,6 +227,8 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
     if (const char *e = getenv("RT_BAND_MIN")) c->band_min = atoll(e) < 0 ? 0 : atoll(e);
+    if (const char *e = getenv("RT_FUSE_MAX")) c->fuse_max = atoll(e) < 0 ? 0 : atoll(e);
+    if (const char *e = getenv("RT_FUSE_LIST")) c->fuse_list = atoll(e) < 0 ? 0 : atoll(e);
     if (const char *e = getenv("RT_BAND_ORDER")) c->band_order = atoi(e) & 3;
     if (const char *e = getenv("RT_BANDS")) c->bands = atoi(e) < 1 ? 1 : (atoi(e) > RT_MAX_BANDS ? RT_MAX_BANDS : atoi(e));
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
@@ -560,7 +569,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.refill_always = c->refill_always;
     L.seg_max = c->seg_max;
     L.blend = cfg->col_weight != 1.0;
-    if (c->split && P > 0) {
+    if (c->split && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).
         // the walk kernels address the lists with 32-bit byte offsets (cand_store): cand_cap * P * 4 < 2^32

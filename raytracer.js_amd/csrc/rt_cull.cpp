@@ -103,6 +103,7 @@ struct Builder {
     std::vector<int> order;     // output slot order (indices into items)
     std::vector<Item> *items;
     bool sah;
+    int leaf;                   // entities per leaf at most (RT_BVH_LEAF, 1..15)
     double clampv;              // SAH area clamp (scene scale)
     std::vector<double> right_area;
 
@@ -156,9 +157,9 @@ struct Builder {
         }
         RtBvh node;
         for (int i = 0; i < 3; i++) { node.lo[i] = round_down(lo[i]); node.hi[i] = round_up(hi[i]); }
-        if (e - b == 1) {
-            node.info = ((int)order.size() << 4) | 1;     // leaf: first prim slot << 4 | count
-            order.push_back(b);
+        if (e - b <= leaf) {
+            node.info = ((int)order.size() << 4) | (e - b);   // leaf: first prim slot << 4 | count
+            for (int k = b; k < e; k++) order.push_back(k);
         } else {
             int mid;
             if (sah) {
@@ -196,13 +197,14 @@ void rt_cull_scale(const double root_pos[3], double root_size, double *delta, do
     *clampv = 4 * scale;
 }
 
-// One node's cull hierarchy.  `recs` are the node's c prim records in Set order (rank already
+// One node's cull hierarchy (leaves of at most `leaf` entities).  `recs` are the node's c prim records in Set order (rank already
 // set); prim_out[0..c) receives them in cull (leaf) order, bvh_out[0..2c-1) the hierarchy, with
 // absolute prim slots (prim_base + k) in leaves and absolute skip pointers (bvh_base + i, -1 past
 // the end).  prefix_out[4k..4k+2] = #sph/#box/#tri among Set positions 0..k (stats).
 int rt_build_node_cull(const RtPrim *recs, int c, int prim_base, int bvh_base, double delta, double clampv,
-                       bool sah, RtPrim *prim_out, RtBvh *bvh_out, int32_t *prefix_out)
+                       bool sah, int leaf, RtPrim *prim_out, RtBvh *bvh_out, int32_t *prefix_out)
 {
+    leaf = leaf < 1 ? 1 : (leaf > 15 ? 15 : leaf);
     int cnt[3] = {0, 0, 0};
     for (int k = 0; k < c; k++) {
         cnt[recs[k].meta & 3]++;
@@ -217,7 +219,7 @@ int rt_build_node_cull(const RtPrim *recs, int c, int prim_base, int bvh_base, d
     }
     std::vector<RtBvh> bvh;
     bvh.reserve(2 * (size_t)c - 1);
-    Builder B{&bvh, {}, &items, sah, clampv, {}};
+    Builder B{&bvh, {}, &items, sah, leaf, clampv, {}};
     B.order.reserve(c);
     B.emit(0, c);
     const int end = (int)bvh.size();

@@ -967,9 +967,14 @@ __device__ int node_first_hit(const RtDevScene &S, const int4 ne, const double o
         // start at its first child (DFS layout: root + 1), or at the single prim of a leaf root
         int i = ne.z;
         if (root_hit) {
-            if (ne.y == 1) {
-                c.exact++;
-                if (prim_hit(S.prim[ne.x], o, d, h)) { best_rank = S.prim[ne.x].rank; best_slot = ne.x; }
+            if (ne.y <= S.bvh_leaf) {                  // the root is the only leaf: its prims in order
+                for (int j = 0; j < ne.y; j++) {
+                    const int slot = ne.x + j;
+                    const int rk = S.prim[slot].rank;
+                    if (rk >= best_rank) continue;
+                    c.exact++;
+                    if (prim_hit(S.prim[slot], o, d, h)) { best_rank = rk; best_slot = slot; }
+                }
                 i = -1;
             } else {
                 i = ne.z + 1;

@@ -31,7 +31,7 @@
 
 void rt_cull_scale(const double root_pos[3], double root_size, double *delta, double *clampv);
 int rt_build_node_cull(const RtPrim *recs, int c, int prim_base, int bvh_base, double delta, double clampv,
-                       bool sah, RtPrim *prim_out, RtBvh *bvh_out, int32_t *prefix_out);
+                       bool sah, int leaf, RtPrim *prim_out, RtBvh *bvh_out, int32_t *prefix_out);
 
 #define HIP_TRY(x)                                                                                \
     do {                                                                                          \
@@ -304,6 +304,7 @@ struct RtSceneStore {
     // breadth-first order (n_top of them), so the walk kernels can stage them in LDS
     int top_levels = 0;
     int32_t n_top = 0;
+    int leaf = 1;                                      // cull-hierarchy leaf size (RT_BVH_LEAF, 1..15)
     std::vector<int32_t> m_list;                       // 1 / list-pool entry
     std::vector<int32_t> m_type, m_shade, m_sub;       // 1 / entity
     std::vector<double> m_geom;                        // 9 / entity
@@ -503,6 +504,7 @@ struct RtSceneStore {
         d.n_subs = n_subs;
         d.n_bvh = (int32_t)bvh_used;
         d.n_top = n_top;
+        d.bvh_leaf = leaf;
         d.n_lds = 0;                                   // set per launch for the walk kernels (rt_kernels.hip)
 #ifdef RT_NO_EXACT_SLOTS
         d.exact_slots = 0;                             // A/B builds: the general plane computation only
@@ -623,7 +625,7 @@ struct RtSceneStore {
                 m_list[lb + k] = s->list_entity[b + k];
                 recs[k] = make_rec(s, s->list_entity[b + k], (int)(lb + k));
             }
-            const int broot = c ? rt_build_node_cull(recs.data(), c, (int)lb, (int)bb, delta, clampv, sah,
+            const int broot = c ? rt_build_node_cull(recs.data(), c, (int)lb, (int)bb, delta, clampv, sah, leaf,
                                                      &prim[lb], &bvh[bb], &prefix[4 * lb])
                                 : -1;
             slots[n] = {(int32_t)lb, c, c, (int32_t)bb, c ? 2 * c - 1 : 0, broot};
@@ -787,7 +789,7 @@ struct RtSceneStore {
                 recs[k] = make_rec(s, s->list_entity[b + k], S.lbeg + k);
             }
             S.cnt = c;
-            S.broot = c ? rt_build_node_cull(recs.data(), c, S.lbeg, S.bbeg, delta, clampv, sah, prim.data(),
+            S.broot = c ? rt_build_node_cull(recs.data(), c, S.lbeg, S.bbeg, delta, clampv, sah, leaf, prim.data(),
                                              bvh.data(), prefix.data())
                         : -1;
             add(A_PRIM, sizeof(RtPrim) * (size_t)S.lbeg, prim.data(), sizeof(RtPrim) * (size_t)c);
@@ -960,7 +962,7 @@ struct RtSceneStore {
             prefix.resize(4 * (size_t)c);
             for (int i = 0; i < c; i++)
                 recs[i] = make_rec_raw(e.set_type[b0 + i], &e.set_geom[9 * (size_t)(b0 + i)], e.set_shade[b0 + i], S.lbeg + i);
-            S.broot = c ? rt_build_node_cull(recs.data(), c, S.lbeg, S.bbeg, delta, clampv, sah, prim.data(), bvh.data(),
+            S.broot = c ? rt_build_node_cull(recs.data(), c, S.lbeg, S.bbeg, delta, clampv, sah, leaf, prim.data(), bvh.data(),
                                              prefix.data())
                         : -1;
             add(A_PRIM, sizeof(RtPrim) * (size_t)S.lbeg, prim.data(), sizeof(RtPrim) * (size_t)c);
@@ -1063,6 +1065,7 @@ RtSceneStore *rt_store_new(bool sah, int ndev, const int *devs, void *const *str
     st->sah = sah;
     st->ndev = ndev;
     if (const char *e = getenv("RT_TOP_LEVELS")) st->top_levels = atoi(e) < 0 ? 0 : (atoi(e) > 8 ? 8 : atoi(e));
+    if (const char *e = getenv("RT_BVH_LEAF")) st->leaf = atoi(e) < 1 ? 1 : (atoi(e) > 15 ? 15 : atoi(e));
     for (int k = 0; k < ndev; k++) {
         st->devs[k] = devs[k];
         st->sts[k] = (hipStream_t)streams[k];

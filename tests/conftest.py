@@ -9,6 +9,12 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# Frames of up to RT_FUSE_MAX pixels (default 2^17) run the fused one-kernel trace.
+# Most parity tests render small frames; they set the threshold to 0 so that they exercise the split
+# walk / first-hit / shade passes that every large frame runs.  Tests of the small-frame default
+# (test_small_frames_fused_default_equals_oracle) create their contexts with it restored.
+os.environ.setdefault("RT_FUSE_MAX", "0")
 for p in (ROOT, os.path.join(ROOT, "raytracer.js_amd", "python"), os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)

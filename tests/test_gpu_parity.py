@@ -550,3 +550,18 @@ def test_top_levels_layout_equals_oracle(top, monkeypatch):
             assert got["stats"].counters() == ref["counters"]
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("wh", [(128, 128), (256, 256), (160, 120)])
+def test_small_frames_fused_default_equals_oracle(wh, monkeypatch):
+    """The shipped default for small frames (RT_FUSE_MAX = 2^17 pixels): one fused
+    k_trace launch instead of the split passes; frames and counters equal the oracle's."""
+    monkeypatch.delenv("RT_FUSE_MAX", raising=False)
+    c = rtamd.Context(0)
+    try:
+        for spec, refmax in ((scenes.config1_spheres(), 2), (scenes.small_random(3), 4)):
+            ref, got = _run_both(c, spec, scenes.make_camera(*wh), scenes.make_config(refmax))
+            _compare(ref, got)
+            assert got["stats"].counters() == ref["counters"]
+    finally:
+        c.close()

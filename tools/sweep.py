@@ -18,7 +18,7 @@ import rtamd  # noqa: E402
 from rtamd import scenes  # noqa: E402
 
 KNOBS = ("RT_OCC", "RT_DIAG", "RT_NO_CULL", "RT_BVH_SAH", "RT_SPLIT", "RT_CAND_CAP", "RT_CONT_GROUP", "RT_SPLIT_LEVELS",
-         "RT_CLAIM_CHUNK", "RT_XCD", "RT_SHADE_OCC", "RT_SEG", "RT_SKIP", "RT_DERIVED", "RT_REFILL", "RT_LV_BLOCKS", "RT_SEG_MAX", "RT_REFILL_ALWAYS", "RT_TOP_LEVELS")
+         "RT_CLAIM_CHUNK", "RT_XCD", "RT_SHADE_OCC", "RT_SEG", "RT_SKIP", "RT_DERIVED", "RT_REFILL", "RT_LV_BLOCKS", "RT_SEG_MAX", "RT_REFILL_ALWAYS", "RT_TOP_LEVELS", "RT_BVH_LEAF", "RT_FUSE_MAX")
 
 
 def main():
