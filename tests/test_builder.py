@@ -78,3 +78,41 @@ def test_builder_outside_growth_reported():
     with pytest.raises(rtamd.RtError) as ei:
         rtamd.build_scene(spec)
     assert ei.value.code == abi.RT_E_TREE
+
+
+# ---- a third restatement, in JavaScript (tests/js/refshape.js add_entity_to_octree) ---------------------
+@pytest.mark.parametrize("name", ["config1", "small1", "small4", "config2", "config3"])
+def test_js_restatement_builds_the_same_tree(tmp_path, name):
+    """The test fixture's add_entity_to_octree (JS, written from src/octree_entity.ts:56-188 apart
+    from the native builder and the C oracle), linearised by the drop-in's serialize_scene, equals
+    the native builder's tree bit for bit (positions, sizes, parents, children, Set-order lists)."""
+    import json
+    import os
+    import shutil
+    import subprocess
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("node not installed")
+    spec = {"config1": scenes.config1_spheres, "small1": lambda: scenes.small_random(1),
+            "small4": lambda: scenes.small_random(4), "config2": scenes.config2, "config3": scenes.config3}[name]()
+    ents = [dict(type=int(e["type"]), geom=[float(x) for x in e["geom"]], depth=int(e["max_in_depth"]))
+            for e in spec.entities]
+    assert all(int(e["max_out_depth"]) == 0 for e in spec.entities)
+    src = tmp_path / "ents.json"
+    src.write_text(json.dumps(dict(root_pos=list(spec.root_pos), root_size=float(spec.root_size), ents=ents)))
+    out = tmp_path / "tree.json"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([node, os.path.join(root, "tests", "js", "build_check.js"), str(src), str(out)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    js = json.loads(out.read_text())
+    got = rtamd.build_scene(spec)
+    n = got.n_nodes
+    assert len(js["node_size"]) == n
+    assert np.array_equal(np.array(js["node_pos"]).view(np.uint64), got.node_pos.reshape(-1).view(np.uint64))
+    assert np.array_equal(np.array(js["node_size"]).view(np.uint64), got.node_size.view(np.uint64))
+    assert np.array_equal(np.array(js["node_parent"]), got.node_parent)
+    assert np.array_equal(np.array(js["node_child"]).reshape(n, 8), got.node_child.reshape(n, 8))
+    assert np.array_equal(np.array(js["node_ent_begin"]), got.node_ent_begin)
+    assert np.array_equal(np.array(js["node_ent_count"]), got.node_ent_count)
+    assert np.array_equal(np.array(js["list_entity"]), got.list_entity)
