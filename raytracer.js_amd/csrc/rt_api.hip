@@ -134,10 +134,11 @@ struct rt_ctx {
     // Small frames of light scenes run the fused k_trace: one launch instead of ~10.  RT_FUSE_MAX: parts
     // of at most this many pixels; RT_FUSE_LIST: scenes of at most this many list entries (the fused
     // loop pays every wave's slowest entity tests at every stop, so heavy scenes keep the split
-    // passes at any size).  Config 1, 256^2: 0.45 -> 0.17 ms; config 3's scene at 128^2: fused 2.2x
-    // slower.
+    // passes at any size).  Config 1, 256^2: 0.45 -> 0.17 ms; 250 entities at 256^2: fused 4 % slower;
+    // config 3's scene at 128^2: fused 2.2x slower.  The reference's demo scene
+    // (src/main.ts:393-396) holds 17 entities.
     int64_t fuse_max = 1 << 18;
-    int64_t fuse_list = 4096;
+    int64_t fuse_list = 64;
     int64_t band_min = 1 << 20;      // RT_BAND_MIN: frames of fewer pixels run as one launch (256^2: 0.44 ms
                                      // one launch against 0.61 in 2 bands; 1080p and up gain, §5.14)
     int n_band = 0;                  // band states initialised

@@ -932,10 +932,15 @@ __device__ __forceinline__ bool ray_box(const RtBvh &b, const RayBox &rb)
     return tmin <= tmax;
 }
 
+// RT_EMIT_BOX = 0 (A/B variant): the walk pass keeps every node with entities and the first-hit pass
+// tests the cull-root box itself (the walker's trips lose the slab test, the lists grow)
+#ifndef RT_EMIT_BOX
+#define RT_EMIT_BOX 1
+#endif
 __device__ __forceinline__ bool node_candidate(const RtDevScene &S, int n, bool cull, const RayBox &rb)
 {
     if (ld_node<int32_t>(S, n, NODE_NENT) == 0) return false;
-    if (!cull || !rb.ok) return true;
+    if (!RT_EMIT_BOX || !cull || !rb.ok) return true;
     const float4 lo = ld_node<float4>(S, n, NODE_BOX);              // lo.xyz, hi.x
     const float2 hi = ld_node<float2>(S, n, NODE_BOX + 16);         // hi.yz
     RtBvh b;
@@ -1748,7 +1753,7 @@ __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
                 Hit h;
                 int rank;
                 long long box = 0;
-                const int hk = node_first_hit<false>(S, ent, o, d, rb, L.cull != 0, c, box, h, rank, true);
+                const int hk = node_first_hit<false>(S, ent, o, d, rb, L.cull != 0, c, box, h, rank, RT_EMIT_BOX != 0);
                 if (hk >= 0) { res = make_int2(node, hk); break; }
             }
         }
@@ -1965,7 +1970,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
                 int rank;
                 long long box = 0;
                 const int hk = node_first_hit<false>(S, make_int4(ent.y, ent.x, ent.z, 0), src.o, src.d, rb,
-                                                     L.cull != 0, c, box, h, rank, true);
+                                                     L.cull != 0, c, box, h, rank, RT_EMIT_BOX != 0);
                 if (hk >= 0) { res = make_int2(node, hk); break; }
                 node = nxt;
                 nxt = nxt2;
@@ -1979,7 +1984,8 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
                 Hit h;
                 int rank;
                 long long box = 0;
-                const int hk = node_first_hit<false>(S, ent, src.o, src.d, rb, L.cull != 0, c, box, h, rank, true);
+                const int hk = node_first_hit<false>(S, ent, src.o, src.d, rb, L.cull != 0, c, box, h, rank,
+                                                     RT_EMIT_BOX != 0);
                 if (hk >= 0) { res = make_int2(node, hk); break; }
             }
 #endif

@@ -554,8 +554,9 @@ def test_top_levels_layout_equals_oracle(top, monkeypatch):
 
 @pytest.mark.parametrize("wh", [(128, 128), (256, 256), (160, 120)])
 def test_small_frames_fused_default_equals_oracle(wh, monkeypatch):
-    """The shipped default for small frames (RT_FUSE_MAX = 2^17 pixels): one fused
-    k_trace launch instead of the split passes; frames and counters equal the oracle's."""
+    """The shipped defaults for small frames: config 1 (9 list entries, within
+    RT_FUSE_LIST) runs one fused k_trace launch, the 250-entity scene the split passes; frames and
+    counters equal the oracle's either way."""
     monkeypatch.delenv("RT_FUSE_MAX", raising=False)
     c = rtamd.Context(0)
     try:

@@ -11,3 +11,4 @@ timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 --profile-out 
 echo "command: python3 bench.py --gpus 1 --steps 20 --warmup 5 --profile-out $OUT/prof3; wall $(( $(date +%s) - T0 )) s" > $OUT/driver_cmd_wall.txt
 timeout -k 10 400 python3 bench.py --config config5 --no-js --cpu-budget 0 --profile-out $OUT/prof5 > $OUT/bench_config5.log 2>&1 || exit $?
 timeout -k 10 200 python3 bench.py --config config1 --no-js --cpu-budget 0 > $OUT/bench_config1.log 2>&1 || exit $?
+OUT=$OUT/ab_nobox CASES="base=: nobox=raytracer.js_amd/lib/librt_amd_nobox.so:" timeout -k 10 400 bash tools/ab_lds.sh > $OUT/ab_nobox.txt 2>&1 || exit $?
