@@ -88,9 +88,9 @@ PASS_BYTES = {"walk": dict(n_ret=48, n_slot=32, n_loc=40), "first": dict(n_cull=
 BYTES_KERNEL = dict(n_ret=48, n_slot=32, n_loc=40, n_cull=32, n_exact=80, n_hit=44, primary=36)
 BYTES_REF = dict(n_ret=48, n_slot=32, n_loc=40, n_sph=36, n_box=36, n_tri=76, n_hit=40, primary=12)
 KERNEL_PASS = {"k_walk": "walk", "k_walk_seg": "walk", "k_walk_refill": "walk", "k_first": "first",
-               "k_first_seg": "first", "k_shade": "shade"}
-TRACE_KERNELS = ("k_walk", "k_walk_seg", "k_walk_refill", "k_first", "k_first_seg", "k_shade", "k_cont", "k_trace",
-                 "k_frame_start")
+               "k_first_seg": "first", "k_first_refill": "first", "k_shade": "shade"}
+TRACE_KERNELS = ("k_walk", "k_walk_seg", "k_walk_refill", "k_first", "k_first_seg", "k_first_refill", "k_shade",
+                 "k_cont", "k_trace", "k_frame_start")
 PMC_FRAMES = 4                 # frames the --pmc-child run profiles (after one warm-up frame)
 PMC_PASSES = {
     "fetch": ["FETCH_SIZE"],

@@ -1787,6 +1787,12 @@ __device__ __forceinline__ bool refill_level(const RtLaunch &L)
     return L.refill > 0 && L.level >= 1 && !seg_mode(L) && cont_g(L) == 64;
 }
 
+#ifndef RT_REFILL_FAST
+#define RT_REFILL_FAST 0              // the fast-ray trip in the refill walk: measured neutral (§5.16)
+#endif
+#ifndef RT_REFILL_OCC
+#define RT_REFILL_OCC 4               // waves per SIMD the refill walk's registers must admit
+#endif
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
 {
@@ -1833,7 +1839,14 @@ __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
             if (n < L.cand_cap) cand_store(L.cand, n, (uint32_t)stride, (uint32_t)q, node);
             n++;
         };
+#if RT_REFILL_FAST
+        // a wave whose walking lanes all have fast rays (all of them in practice) runs the trip
+        // without the exact six-division slot exit, as k_walk's fast loop does
+        if (__all(w.fast || res != 1)) walker_trip<false, true>(S, w, emit, -1, res);
+        else walker_trip<false, false>(S, w, emit, -1, res);
+#else
         walker_trip<false, false>(S, w, emit, -1, res);
+#endif
         if (res != 1 && res != IDLE) {
             const int end = res == 0 ? 0 : (res == -2 ? 2 : 1);
             L.cand_n[q] = n > L.cand_cap ? -1 : n * 4 + end;
@@ -1933,6 +1946,77 @@ __device__ __forceinline__ bool early_shade(const RtLaunch &L, const RaySrc &src
 #ifndef RT_FIRST_PIPE
 #define RT_FIRST_PIPE 0
 #endif
+#ifndef RT_FIRST_REFILL
+#define RT_FIRST_REFILL 0              // measured slower: lanes refilled with new rays
+#endif                                 // lose the cache locality of the rays a wave already holds
+
+// First-hit pass of a wide bounce level with per-lane refill (the levels k_walk_refill walks): a
+// lane tests one candidate node per trip; a lane whose ray is done (a hit, or its list exhausted)
+// writes first[q] and, once L.refill lanes of the wave are idle, they take the next rays of the
+// level's queue with one atomic.  Each ray's candidates are tested in list order with the same
+// node_first_hit as k_first, so first[] is identical; the rays of such a level are incoherent and
+// their lists differ in length, so a wave of 64 no longer waits for its longest list.
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_first_refill(RtLaunch L)
+{
+    if (!RT_FIRST_REFILL || !refill_level(L)) return;
+    const int lane = threadIdx.x & 63;
+    const RtDevScene &S = L.scene;
+    const uint32_t stride = (uint32_t)((size_t)L.rows * (size_t)L.cam.width);
+    const int n_rays = *lvl_ctr(L, L.level - 1);
+    int32_t *head = pass_heads(L, L.level, 2);
+    const bool fault = L.setup->fault != 0;
+    const RtCont *queue = L.queue[(L.level - 1) & 1];
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int q = 0, k = 0, n = 0;
+    bool busy = false, drained = false;
+    double o[3] = {0, 0, 0}, d[3] = {0, 0, 0};
+    RayBox rb{};
+    const unsigned long long below = (1ull << lane) - 1;
+    for (;;) {
+        const unsigned long long m_busy = __ballot(busy);
+        const int idle = 64 - __popcll(m_busy);
+        if (!drained && (idle >= L.refill || !m_busy)) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(head, idle);
+            base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
+            drained = base + idle >= n_rays;
+            const int r = base + __popcll(~m_busy & below);
+            if (!busy && r < n_rays) {
+                q = r;
+                const int cn = L.cand_n[q];
+                if (cn >= 4 && !fault) {
+                    const RtCont *rec = queue + q;
+                    for (int i = 0; i < 3; i++) { o[i] = rec->o[i]; d[i] = rec->d[i]; }
+                    rb = make_raybox(o, d);
+                    n = cn >> 2;
+                    k = 0;
+                    busy = true;
+                } else {
+                    reinterpret_cast<int2 *>(L.first)[q] = make_int2(-1, -1);
+                }
+            }
+        }
+        if (!__ballot(busy)) {
+            if (drained) break;
+            continue;
+        }
+        if (busy) {
+            const int node = cand_load(L.cand, k, stride, (uint32_t)q);
+            const int4 hdr = ld_node<int4>(S, node, NODE_NENT);      // {n_ent, ent_begin, bvh_root, -}
+            Hit h;
+            int rank;
+            long long box = 0;
+            const int hk = node_first_hit<false>(S, make_int4(hdr.y, hdr.x, hdr.z, 0), o, d, rb, L.cull != 0, c, box,
+                                                 h, rank, RT_EMIT_BOX != 0);
+            k++;
+            if (hk >= 0 || k >= n) {
+                reinterpret_cast<int2 *>(L.first)[q] = hk >= 0 ? make_int2(node, hk) : make_int2(-1, -1);
+                busy = false;
+            }
+        }
+    }
+}
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
 {
@@ -1943,6 +2027,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
     const bool fault = L.setup->fault != 0;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (seg_mode(L)) return;                          // k_first_seg takes this level
+    if (RT_FIRST_REFILL && refill_level(L)) return;   // k_first_refill takes this level
     const int ch = L.claim_chunk;
     for (;;) {
         int t_end;
@@ -2211,9 +2296,10 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
             if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lw, mb, lds);   // one of the two runs (§5.10)
-            if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<4>, st, Lw, mb, lds);
+            if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<RT_REFILL_OCC>, st, Lw, mb, lds);
             launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
+            if (RT_FIRST_REFILL && lv >= 1 && Lv.refill > 0) launch_persistent(k_first_refill<6>, st, Lv, mb);
             if (lv >= 1 && L.seg > 1) launch_persistent(k_first_seg<4>, st, Lv, mb);
             launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv, mb);
             HIP_TRY(hipGetLastError());

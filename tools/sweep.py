@@ -44,8 +44,10 @@ def main():
         ctx.upload(scene)
         _, st = ctx.trace_rows_device(cam, cfg, 0, 1, H, buf.data_ptr(), s.cuda_stream, stats=True)
         for _ in range(2):
+            # each warm-up frame finishes before the next starts, so its work counters become the
+            # grid hints / refill choices of the timed frames (the bench's steady state)
             ctx.trace_rows_device(cam, cfg, 0, 1, H, buf.data_ptr(), s.cuda_stream)
-        s.synchronize()
+            s.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.frames):
             ctx.trace_rows_device(cam, cfg, 0, 1, H, buf.data_ptr(), s.cuda_stream)
