@@ -1855,6 +1855,37 @@ __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
     }
 }
 
+// The walk pass's work for one ray (k_walk, k_walk_first): its OctreeWalker stops filtered to the
+// candidate list, and cand_n = count * 4 + end (or -1 on overflow), which it also returns.
+__device__ __forceinline__ int walk_item(const RtLaunch &L, const RtDevScene &S, const RtFrameSetup &F,
+                                         const RaySrc &src, size_t stride, Counters &c)
+{
+    const RayBox rb = make_raybox(src.o, src.d);
+    Walker w;
+    int n = 0, end = 0;
+    const bool seated = src.rec ? walker_set(S, w, src.o, src.d, false, 0, 0, c) >= 0
+                                : !F.fault && walker_set(S, w, src.o, src.d, F.start_tree >= 0, F.start_tree,
+                                                         F.start_oct, c) >= 0;
+    if (!seated) {
+        end = src.rec ? 3 : 1;
+    } else {
+        auto emit = [&](int node) {
+            if (!node_candidate(S, node, L.cull != 0, rb)) return;
+            if (n < L.cand_cap) cand_store(L.cand, n, (uint32_t)stride, (uint32_t)src.id, node);
+            n++;
+        };
+        const int r = walker_run<false, true>(S, w, emit);
+        if (r < 0) end = r == -2 ? 2 : 1;
+    }
+    const int cn = n > L.cand_cap ? -1 : n * 4 + end;
+    L.cand_n[src.id] = cn;
+    return cn;
+}
+
+#ifndef RT_WALK_FIRST
+#define RT_WALK_FIRST 0
+#endif
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
 {
@@ -1865,6 +1896,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (seg_mode(L) || refill_level(L)) return;       // k_walk_seg / k_walk_refill take this level
+    if (RT_WALK_FIRST && L.level == 0) return;        // k_walk_first takes level 0
     stage_top(S);
     for (;;) {
         int t_end;
@@ -1873,24 +1905,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
         RaySrc src;
         ray_src(L, t, lane, src);
         if (!src.valid) continue;
-        const RayBox rb = make_raybox(src.o, src.d);
-        Walker w;
-        int n = 0, end = 0;
-        const bool seated = src.rec ? walker_set(S, w, src.o, src.d, false, 0, 0, c) >= 0
-                                    : !F.fault && walker_set(S, w, src.o, src.d, F.start_tree >= 0, F.start_tree,
-                                                             F.start_oct, c) >= 0;
-        if (!seated) {
-            end = src.rec ? 3 : 1;
-        } else {
-            auto emit = [&](int node) {
-                if (!node_candidate(S, node, L.cull != 0, rb)) return;
-                if (n < L.cand_cap) cand_store(L.cand, n, (uint32_t)stride, (uint32_t)src.id, node);
-                n++;
-            };
-            const int r = walker_run<false, true>(S, w, emit);
-            if (r < 0) end = r == -2 ? 2 : 1;
-        }
-        L.cand_n[src.id] = n > L.cand_cap ? -1 : n * 4 + end;
+        walk_item(L, S, F, src, stride, c);
     }
 }
 
@@ -1943,9 +1958,6 @@ __device__ __forceinline__ bool early_shade(const RtLaunch &L, const RaySrc &src
     return true;
 }
 
-#ifndef RT_FIRST_PIPE
-#define RT_FIRST_PIPE 0
-#endif
 #ifndef RT_FIRST_REFILL
 #define RT_FIRST_REFILL 0              // measured slower: lanes refilled with new rays
 #endif                                 // lose the cache locality of the rays a wave already holds
@@ -2017,6 +2029,38 @@ __global__ void __launch_bounds__(256, MINW) k_first_refill(RtLaunch L)
         }
     }
 }
+// The first-hit pass's work for one ray (k_first, k_walk_first): the first candidate of its list
+// (walk order) with an exact hit; at level 0 the plain terminal rays end here (early_shade) and the
+// others are queued for k_shade.
+__device__ __forceinline__ void first_item(const RtLaunch &L, const RtDevScene &S, const RaySrc &src, int cn,
+                                           uint32_t stride, bool fault, Counters &c)
+{
+    int2 res = make_int2(-1, -1);
+    if (cn >= 4 && !fault) {
+        const RayBox rb = make_raybox(src.o, src.d);
+        const int n = cn >> 2;
+        for (int k = 0; k < n; k++) {
+            const int node = cand_load(L.cand, k, stride, (uint32_t)src.id);
+            const RtNode &nd = S.node[node];               // the line k_walk read for this candidate
+            const int4 ent = make_int4(nd.ent_begin, nd.n_ent, nd.bvh_root, 0);
+            Hit h;
+            int rank;
+            long long box = 0;
+            const int hk = node_first_hit<false>(S, ent, src.o, src.d, rb, L.cull != 0, c, box, h, rank,
+                                                 RT_EMIT_BOX != 0);
+            if (hk >= 0) { res = make_int2(node, hk); break; }
+        }
+    }
+    if (RT_EARLY_SHADE && L.level == 0) {
+        // level 0: end the plain terminal rays here; queue the rest for k_shade (ray_cn is free at
+        // level 0), wave by wave so a shading wave keeps a tile's rays together
+        RayResult R;
+        if (!(cn >= 0 && !fault && early_shade(L, src, cn, res, R))) L.ray_cn[wave_reserve(shade_n(L))] = (int)src.id;
+        else write_pixel(L, (size_t)src.pix, R);
+    }
+    reinterpret_cast<int2 *>(L.first)[src.id] = res;
+}
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
 {
@@ -2028,62 +2072,43 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (seg_mode(L)) return;                          // k_first_seg takes this level
     if (RT_FIRST_REFILL && refill_level(L)) return;   // k_first_refill takes this level
+    if (RT_WALK_FIRST && L.level == 0) return;        // k_walk_first took level 0
     const int ch = L.claim_chunk;
     for (;;) {
         int t_end;
         const int t0 = claim_xcd(pass_heads(L, L.level, 2), items, lane, ch, t_end, L.xcd_mask & 2);
         if (t0 >= items) break;
         for (int t = t0; t < t_end; t++) {
+            RaySrc src;
+            ray_src(L, t, lane, src);
+            if (!src.valid) continue;
+            first_item(L, S, src, L.cand_n[src.id], (uint32_t)stride, fault, c);
+        }
+    }
+}
+
+// Level 0 as one pass (RT_WALK_FIRST): per 8x8 tile a wave walks its rays, then runs
+// their first-hit tests at once, from lists it has just written (cache-resident), so a CU interleaves
+// walking waves (VALU-bound) with testing waves (latency-bound) instead of running the two passes
+// one after the other.  Same walk, same lists, same tests: identical results.
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_walk_first(RtLaunch L)
+{
+    const int lane = threadIdx.x & 63;
+    const int items = n_items(L);
+    const RtFrameSetup F = *L.setup;
+    const RtDevScene &S = L.scene;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (;;) {
+        int t_end;
+        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
+        if (t >= items) break;
         RaySrc src;
         ray_src(L, t, lane, src);
         if (!src.valid) continue;
-        const int cn = L.cand_n[src.id];
-        int2 res = make_int2(-1, -1);
-        if (cn >= 4 && !fault) {
-            const RayBox rb = make_raybox(src.o, src.d);
-            const int n = cn >> 2;
-#if RT_FIRST_PIPE
-            // software pipeline over the list: while candidate k's hierarchy is walked, candidate
-            // k + 1's record header and candidate k + 2's id are already loading
-            int node = cand_load(L.cand, 0, (uint32_t)stride, (uint32_t)src.id);
-            int nxt = n > 1 ? cand_load(L.cand, 1, (uint32_t)stride, (uint32_t)src.id) : 0;
-            int4 ent = ld_node<int4>(S, node, NODE_NENT);        // {n_ent, ent_begin, bvh_root, -}
-            for (int k = 0; k < n; k++) {
-                const int4 ent_n = k + 1 < n ? ld_node<int4>(S, nxt, NODE_NENT) : ent;
-                const int nxt2 = k + 2 < n ? cand_load(L.cand, k + 2, (uint32_t)stride, (uint32_t)src.id) : 0;
-                Hit h;
-                int rank;
-                long long box = 0;
-                const int hk = node_first_hit<false>(S, make_int4(ent.y, ent.x, ent.z, 0), src.o, src.d, rb,
-                                                     L.cull != 0, c, box, h, rank, RT_EMIT_BOX != 0);
-                if (hk >= 0) { res = make_int2(node, hk); break; }
-                node = nxt;
-                nxt = nxt2;
-                ent = ent_n;
-            }
-#else
-            for (int k = 0; k < n; k++) {
-                const int node = cand_load(L.cand, k, (uint32_t)stride, (uint32_t)src.id);
-                const RtNode &nd = S.node[node];               // the line k_walk read for this candidate
-                const int4 ent = make_int4(nd.ent_begin, nd.n_ent, nd.bvh_root, 0);
-                Hit h;
-                int rank;
-                long long box = 0;
-                const int hk = node_first_hit<false>(S, ent, src.o, src.d, rb, L.cull != 0, c, box, h, rank,
-                                                     RT_EMIT_BOX != 0);
-                if (hk >= 0) { res = make_int2(node, hk); break; }
-            }
-#endif
-        }
-        if (RT_EARLY_SHADE && L.level == 0) {
-            // level 0: end the plain terminal rays here; queue the rest for k_shade (ray_cn is free at
-            // level 0), wave by wave so a shading wave keeps a tile's rays together
-            RayResult R;
-            if (!(cn >= 0 && !fault && early_shade(L, src, cn, res, R))) L.ray_cn[wave_reserve(shade_n(L))] = (int)src.id;
-            else write_pixel(L, (size_t)src.pix, R);
-        }
-        reinterpret_cast<int2 *>(L.first)[src.id] = res;
-        }
+        const int cn = walk_item(L, S, F, src, stride, c);
+        first_item(L, S, src, cn, (uint32_t)stride, F.fault != 0, c);
     }
 }
 
@@ -2292,7 +2317,8 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             RtLaunch Lw = Lv;                         // the walk kernels read the upper levels from LDS
             Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
             const size_t lds = sizeof(RtNode) * (size_t)Lw.scene.n_lds;
-            launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb, lds);
+            if (RT_WALK_FIRST && lv == 0) launch_persistent(k_walk_first<4>, st, Lw, mb, lds);
+            else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb, lds);
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
             if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lw, mb, lds);   // one of the two runs (§5.10)
