@@ -89,8 +89,8 @@ BYTES_KERNEL = dict(n_ret=48, n_slot=32, n_loc=40, n_cull=32, n_exact=80, n_hit=
 BYTES_REF = dict(n_ret=48, n_slot=32, n_loc=40, n_sph=36, n_box=36, n_tri=76, n_hit=40, primary=12)
 KERNEL_PASS = {"k_walk": "walk", "k_walk_seg": "walk", "k_walk_refill": "walk", "k_first": "first",
                "k_first_seg": "first", "k_first_refill": "first", "k_shade": "shade"}
-TRACE_KERNELS = ("k_walk", "k_walk_seg", "k_walk_refill", "k_first", "k_first_seg", "k_first_refill", "k_shade",
-                 "k_cont", "k_trace", "k_frame_start")
+TRACE_KERNELS = ("k_walk_first", "k_walk", "k_walk_seg", "k_walk_refill", "k_first", "k_first_seg", "k_first_refill",
+                 "k_shade", "k_cont", "k_trace", "k_frame_start")
 PMC_FRAMES = 4                 # frames the --pmc-child run profiles (after one warm-up frame)
 PMC_PASSES = {
     "fetch": ["FETCH_SIZE"],
@@ -439,6 +439,13 @@ def kernel_rooflines(dur, pmc, counters):
     SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU of 64; HBM: 2*FETCH_SIZE + WRITE_SIZE (KiB; FETCH_SIZE
     doubled on gfx950) over the duration against 8 TB/s; algorithmic bytes (§8(d), cache-served)."""
     out = {}
+    # level 0 as one walk + first-hit kernel (k_walk_first, DESIGN.md §5.18): the walk and first-hit
+    # passes' algorithmic bytes are one pool, shared by their kernels in proportion to time
+    pass_of, pass_bytes = dict(KERNEL_PASS), dict(PASS_BYTES)
+    if "k_walk_first" in dur:
+        pass_of = {k: ("walk+first" if p in ("walk", "first") else p) for k, p in pass_of.items()}
+        pass_of["k_walk_first"] = "walk+first"
+        pass_bytes["walk+first"] = dict(PASS_BYTES["walk"], **PASS_BYTES["first"])
     for k, ms in sorted(dur.items(), key=lambda kv: -kv[1]):
         c = pmc.get(k, {})
         e = dict(ms_per_frame=round(ms, 4))
@@ -461,11 +468,11 @@ def kernel_rooflines(dur, pmc, counters):
             e.update(active_lanes=round(lanes, 2), lane_util=round(lanes / 64, 4))
         if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in c:
             e.update(wait_frac=round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4))
-        p = KERNEL_PASS.get(k)
+        p = pass_of.get(k)
         if p:
             # the pass's algorithmic bytes are shared by its kernels in proportion to their time
-            share = ms / sum(v for kk, v in dur.items() if KERNEL_PASS.get(kk) == p)
-            ab = algorithmic_bytes(counters, PASS_BYTES[p]) * share
+            share = ms / sum(v for kk, v in dur.items() if pass_of.get(kk) == p)
+            ab = algorithmic_bytes(counters, pass_bytes[p]) * share
             e.update(alg_bytes_cache_served=int(ab), alg_GBps=round(ab / s / 1e9, 1))
         roofs = {r: e[f] for r, f in (("valu-issue", "valu_issue_frac"), ("hbm", "hbm_frac")) if f in e}
         if roofs:

@@ -1883,7 +1883,7 @@ __device__ __forceinline__ int walk_item(const RtLaunch &L, const RtDevScene &S,
 }
 
 #ifndef RT_WALK_FIRST
-#define RT_WALK_FIRST 0
+#define RT_WALK_FIRST 1                // level 0 as one walk + first-hit pass
 #endif
 
 template <int MINW>

@@ -10,7 +10,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# Frames of up to RT_FUSE_MAX pixels (default 2^17) run the fused one-kernel trace.
+# Frames of up to RT_FUSE_MAX pixels (default 2^18) of light scenes run the fused one-kernel trace.
 # Most parity tests render small frames; they set the threshold to 0 so that they exercise the split
 # walk / first-hit / shade passes that every large frame runs.  Tests of the small-frame default
 # (test_small_frames_fused_default_equals_oracle) create their contexts with it restored.
