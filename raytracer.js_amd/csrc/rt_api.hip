@@ -139,6 +139,10 @@ struct rt_ctx {
     // (src/main.ts:393-396) holds 17 entities.
     int64_t fuse_max = 1 << 18;
     int64_t fuse_list = 64;
+    // Level 0 of the split path as one walk + first-hit kernel for scenes of at most RT_WF_LIST list
+    // entries: config 3 (101 k entries) 4 % faster; config 5 (1 M) runs its long
+    // candidate scans faster in k_first's own launch (6 waves/SIMD against 4), 17.9 against 18.2 ms.
+    int64_t wf_list = 1 << 19;
     int64_t band_min = 1 << 20;      // RT_BAND_MIN: frames of fewer pixels run as one launch (256^2: 0.44 ms
                                      // one launch against 0.61 in 2 bands; 1080p and up gain, §5.14)
     int n_band = 0;                  // band states initialised
@@ -230,6 +234,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_BAND_MIN")) c->band_min = atoll(e) < 0 ? 0 : atoll(e);
     if (const char *e = getenv("RT_FUSE_MAX")) c->fuse_max = atoll(e) < 0 ? 0 : atoll(e);
     if (const char *e = getenv("RT_FUSE_LIST")) c->fuse_list = atoll(e) < 0 ? 0 : atoll(e);
+    if (const char *e = getenv("RT_WF_LIST")) c->wf_list = atoll(e);
     if (const char *e = getenv("RT_BAND_ORDER")) c->band_order = atoi(e) & 3;
     if (const char *e = getenv("RT_BANDS")) c->bands = atoi(e) < 1 ? 1 : (atoi(e) > RT_MAX_BANDS ? RT_MAX_BANDS : atoi(e));
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
@@ -569,6 +574,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.refill = c->refill;
     L.refill_always = c->refill_always;
     L.seg_max = c->seg_max;
+    L.walk_first = (int64_t)d.scene.n_list <= c->wf_list;
     L.blend = cfg->col_weight != 1.0;
     if (c->split && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot

@@ -205,6 +205,7 @@ struct RtLaunch {
     int32_t refill;                             // wide bounce levels: idle lanes that take new rays (0: off; RT_REFILL)
     int32_t refill_always;                      // refill every wide level, not only where a recent frame had one (tests)
     int32_t seg_max;                            // bounce levels of more rays run unsegmented (0: no limit; RT_SEG_MAX)
+    int32_t walk_first;                         // level 0 as one walk + first-hit kernel (k_walk_first; §5.18)
     const int32_t *ctr_hint;                    // host snapshot of a recent frame's ctr (-1: none yet), or null
     int32_t *ctr_out;                           // pinned: this frame's ctr is copied here at its end (or null)
     void *ctr_done;                             // hipEvent_t recorded after that copy

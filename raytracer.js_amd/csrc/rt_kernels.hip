@@ -150,15 +150,24 @@ __device__ __forceinline__ int4 node_up4(const RtDevScene &S, int n) { return ld
 struct RayBox;
 __device__ __forceinline__ bool node_candidate(const RtDevScene &S, int n, bool cull, const RayBox &rb);
 
-// Candidate lists are k-major [cand_cap][rays] int32; (k * stride + ray) * 4 < 2^32 is ensured by
-// the host (prepare caps cand_cap), so the store address is a 32-bit offset from the uniform base.
-__device__ __forceinline__ void cand_store(int32_t *cand, int k, uint32_t stride, uint32_t ray, int node)
+// Candidate lists are k-major [cand_cap][rays] int32, or ray-major [rays][cand_cap] on the levels
+// RT_CAND_LAYOUT selects (1: bounce levels, 2: every level); cand_cap * rays * 4 < 2^32 is ensured
+// by the host (prepare caps cand_cap), so the address is a 32-bit offset from the uniform base.
+#ifndef RT_CAND_LAYOUT
+#define RT_CAND_LAYOUT 0
+#endif
+__device__ __forceinline__ uint32_t cand_off(const RtLaunch &L, int k, uint32_t stride, uint32_t ray)
 {
-    *reinterpret_cast<int32_t *>(reinterpret_cast<char *>(cand) + (((uint32_t)k * stride + ray) << 2)) = node;
+    const bool rm = RT_CAND_LAYOUT == 2 || (RT_CAND_LAYOUT == 1 && L.level >= 1);
+    return (rm ? ray * (uint32_t)L.cand_cap + (uint32_t)k : (uint32_t)k * stride + ray) << 2;
 }
-__device__ __forceinline__ int cand_load(const int32_t *cand, int k, uint32_t stride, uint32_t ray)
+__device__ __forceinline__ void cand_store(const RtLaunch &L, int k, uint32_t stride, uint32_t ray, int node)
 {
-    return ld_at<int32_t>(cand, ((uint32_t)k * stride + ray) << 2);
+    *reinterpret_cast<int32_t *>(reinterpret_cast<char *>(L.cand) + cand_off(L, k, stride, ray)) = node;
+}
+__device__ __forceinline__ int cand_load(const RtLaunch &L, int k, uint32_t stride, uint32_t ray)
+{
+    return ld_at<int32_t>(L.cand, cand_off(L, k, stride, ray));
 }
 
 // ---- Box.line_intersection (src/math/intersection.ts:150-204) on a cube ----------------------------
@@ -1018,6 +1027,70 @@ __device__ int node_first_hit(const RtDevScene &S, const int4 ne, const double o
     return best_slot;
 }
 
+// A ray's candidate scan (the first-hit pass): the first node of its list, in walk order, with an
+// exact hit, and the winning prim slot — node_first_hit over list[0..n) until one hits.
+// RT_SCAN_FLAT = 1: one loop for the whole scan.  A trip is one cull-hierarchy record, or one leaf
+// prim's exact test, or the step to the next candidate, so a lane whose traversal of one node ended
+// goes on to its next candidate at once instead of waiting, at the end of every node, for the
+// wave's longest traversal (the nested loops pay the sum over candidates of the wave's maximum; this
+// loop the maximum over lanes of each lane's sum).  Same records, same tests in the same order per
+// ray: identical results.  Rays that cannot be culled (rb.ok false) keep the nested scan.
+// k_walk_first keeps the nested scan (FLAT = false): behind the walk in the same wave it measured 1 %
+// faster there.
+#ifndef RT_SCAN_FLAT
+#define RT_SCAN_FLAT 1
+#endif
+template <bool FLAT = true>
+__device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &S, const double o[3], const double d[3],
+                                           const RayBox &rb, uint32_t stride, uint32_t id, int n, Counters &c)
+{
+    int2 res = make_int2(-1, -1);
+    if (!FLAT || !RT_SCAN_FLAT || !(L.cull != 0 && rb.ok)) {
+        for (int k = 0; k < n; k++) {
+            const int node = cand_load(L, k, stride, id);
+            const int4 hdr = ld_node<int4>(S, node, NODE_NENT);      // {n_ent, ent_begin, bvh_root, -}
+            Hit h;
+            int rank;
+            long long box = 0;
+            const int hk = node_first_hit<false>(S, make_int4(hdr.y, hdr.x, hdr.z, 0), o, d, rb, L.cull != 0, c, box,
+                                                 h, rank, RT_EMIT_BOX != 0);
+            if (hk >= 0) { res = make_int2(node, hk); break; }
+        }
+        return res;
+    }
+    // i >= 0: the next record of the current node's hierarchy; slot < prim_end: leaf prims to test
+    int k = 0, node = -1, i = -1, slot = 0, prim_end = 0, best_rank = 0x7fffffff, best_slot = -1;
+    bool active = n > 0;
+    while (active) {
+        if (slot < prim_end) {
+            const int rk = S.prim[slot].rank;
+            if (rk < best_rank) {
+                Hit h;
+                c.exact++;
+                if (prim_hit(S.prim[slot], o, d, h)) { best_rank = rk; best_slot = slot; }
+            }
+            slot++;
+        } else if (i >= 0) {
+            const RtBvh b = S.bvh[i];
+            if (!ray_box(b, rb)) i = b.skip;
+            else if (b.info < 0) i++;
+            else { slot = b.info >> 4; prim_end = slot + (b.info & 15); i = b.skip; }
+        } else if (best_slot >= 0) {                       // the current node has the first hit
+            res = make_int2(node, best_slot);
+            active = false;
+        } else if (k >= n) {
+            active = false;
+        } else {
+            node = cand_load(L, k++, stride, id);
+            const int4 hdr = ld_node<int4>(S, node, NODE_NENT);
+            if (!RT_EMIT_BOX) i = hdr.z;                   // node_first_hit's root_hit: the walk pass
+            else if (hdr.x <= S.bvh_leaf) { slot = hdr.y; prim_end = hdr.y + hdr.x; }   // crossed the
+            else i = hdr.z + 1;                            // root box: a leaf root's prims, or its children
+        }
+    }
+    return res;
+}
+
 // ---- camera scan (src/view/camera.ts:207-250; vector.rotate_vectors src/math/vector.ts:318-323) ----
 __device__ __forceinline__ int part_row_to_y(int lr, int part, int n_parts, int stripe)
 {
@@ -1699,7 +1772,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
             const size_t id = (size_t)q * K + j;
             auto emit = [&](int node) {
                 if (!node_candidate(S, node, L.cull != 0, rb)) return;
-                if (n < L.cand_cap) cand_store(L.cand, n, (uint32_t)stride, (uint32_t)id, node);
+                if (n < L.cand_cap) cand_store(L, n, (uint32_t)stride, (uint32_t)id, node);
                 n++;
             };
             const int r = walker_run<true>(S, w, emit, stop);
@@ -1744,18 +1817,7 @@ __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
         if (valid && open && cn >= 8 && !fault) {
             const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
             const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
-            const RayBox rb = make_raybox(o, d);
-            const int n = cn >> 3;
-            for (int k = 0; k < n; k++) {
-                const int node = cand_load(L.cand, k, (uint32_t)stride, (uint32_t)id);
-                const RtNode &nd = S.node[node];
-                const int4 ent = make_int4(nd.ent_begin, nd.n_ent, nd.bvh_root, 0);
-                Hit h;
-                int rank;
-                long long box = 0;
-                const int hk = node_first_hit<false>(S, ent, o, d, rb, L.cull != 0, c, box, h, rank, RT_EMIT_BOX != 0);
-                if (hk >= 0) { res = make_int2(node, hk); break; }
-            }
+            res = scan_first(L, S, o, d, make_raybox(o, d), (uint32_t)stride, (uint32_t)id, cn >> 3, c);
         }
         // in segment order: overflow -> the whole ray to k_cont; a hit wins; an end ends the ray
         bool done = false;
@@ -1836,7 +1898,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
         }
         auto emit = [&](int node) {
             if (!node_candidate(S, node, L.cull != 0, rb)) return;
-            if (n < L.cand_cap) cand_store(L.cand, n, (uint32_t)stride, (uint32_t)q, node);
+            if (n < L.cand_cap) cand_store(L, n, (uint32_t)stride, (uint32_t)q, node);
             n++;
         };
 #if RT_REFILL_FAST
@@ -1871,7 +1933,7 @@ __device__ __forceinline__ int walk_item(const RtLaunch &L, const RtDevScene &S,
     } else {
         auto emit = [&](int node) {
             if (!node_candidate(S, node, L.cull != 0, rb)) return;
-            if (n < L.cand_cap) cand_store(L.cand, n, (uint32_t)stride, (uint32_t)src.id, node);
+            if (n < L.cand_cap) cand_store(L, n, (uint32_t)stride, (uint32_t)src.id, node);
             n++;
         };
         const int r = walker_run<false, true>(S, w, emit);
@@ -1882,9 +1944,6 @@ __device__ __forceinline__ int walk_item(const RtLaunch &L, const RtDevScene &S,
     return cn;
 }
 
-#ifndef RT_WALK_FIRST
-#define RT_WALK_FIRST 1                // level 0 as one walk + first-hit pass
-#endif
 
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
@@ -1896,7 +1955,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (seg_mode(L) || refill_level(L)) return;       // k_walk_seg / k_walk_refill take this level
-    if (RT_WALK_FIRST && L.level == 0) return;        // k_walk_first takes level 0
+    if (L.walk_first && L.level == 0) return;         // k_walk_first takes level 0
     stage_top(S);
     for (;;) {
         int t_end;
@@ -2014,7 +2073,7 @@ __global__ void __launch_bounds__(256, MINW) k_first_refill(RtLaunch L)
             continue;
         }
         if (busy) {
-            const int node = cand_load(L.cand, k, stride, (uint32_t)q);
+            const int node = cand_load(L, k, stride, (uint32_t)q);
             const int4 hdr = ld_node<int4>(S, node, NODE_NENT);      // {n_ent, ent_begin, bvh_root, -}
             Hit h;
             int rank;
@@ -2032,25 +2091,12 @@ __global__ void __launch_bounds__(256, MINW) k_first_refill(RtLaunch L)
 // The first-hit pass's work for one ray (k_first, k_walk_first): the first candidate of its list
 // (walk order) with an exact hit; at level 0 the plain terminal rays end here (early_shade) and the
 // others are queued for k_shade.
+template <bool FLAT = true>
 __device__ __forceinline__ void first_item(const RtLaunch &L, const RtDevScene &S, const RaySrc &src, int cn,
                                            uint32_t stride, bool fault, Counters &c)
 {
     int2 res = make_int2(-1, -1);
-    if (cn >= 4 && !fault) {
-        const RayBox rb = make_raybox(src.o, src.d);
-        const int n = cn >> 2;
-        for (int k = 0; k < n; k++) {
-            const int node = cand_load(L.cand, k, stride, (uint32_t)src.id);
-            const RtNode &nd = S.node[node];               // the line k_walk read for this candidate
-            const int4 ent = make_int4(nd.ent_begin, nd.n_ent, nd.bvh_root, 0);
-            Hit h;
-            int rank;
-            long long box = 0;
-            const int hk = node_first_hit<false>(S, ent, src.o, src.d, rb, L.cull != 0, c, box, h, rank,
-                                                 RT_EMIT_BOX != 0);
-            if (hk >= 0) { res = make_int2(node, hk); break; }
-        }
-    }
+    if (cn >= 4 && !fault) res = scan_first<FLAT>(L, S, src.o, src.d, make_raybox(src.o, src.d), stride, (uint32_t)src.id, cn >> 2, c);
     if (RT_EARLY_SHADE && L.level == 0) {
         // level 0: end the plain terminal rays here; queue the rest for k_shade (ray_cn is free at
         // level 0), wave by wave so a shading wave keeps a tile's rays together
@@ -2072,7 +2118,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (seg_mode(L)) return;                          // k_first_seg takes this level
     if (RT_FIRST_REFILL && refill_level(L)) return;   // k_first_refill takes this level
-    if (RT_WALK_FIRST && L.level == 0) return;        // k_walk_first took level 0
+    if (L.walk_first && L.level == 0) return;         // k_walk_first took level 0
     const int ch = L.claim_chunk;
     for (;;) {
         int t_end;
@@ -2087,7 +2133,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
     }
 }
 
-// Level 0 as one pass (RT_WALK_FIRST): per 8x8 tile a wave walks its rays, then runs
+// Level 0 as one pass (L.walk_first: scenes of at most RT_WF_LIST list entries): per 8x8 tile a wave walks its rays, then runs
 // their first-hit tests at once, from lists it has just written (cache-resident), so a CU interleaves
 // walking waves (VALU-bound) with testing waves (latency-bound) instead of running the two passes
 // one after the other.  Same walk, same lists, same tests: identical results.
@@ -2100,6 +2146,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_first(RtLaunch L)
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    stage_top(S);
     for (;;) {
         int t_end;
         const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
@@ -2108,7 +2155,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_first(RtLaunch L)
         ray_src(L, t, lane, src);
         if (!src.valid) continue;
         const int cn = walk_item(L, S, F, src, stride, c);
-        first_item(L, S, src, cn, (uint32_t)stride, F.fault != 0, c);
+        first_item<false>(L, S, src, cn, (uint32_t)stride, F.fault != 0, c);
     }
 }
 
@@ -2317,7 +2364,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             RtLaunch Lw = Lv;                         // the walk kernels read the upper levels from LDS
             Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
             const size_t lds = sizeof(RtNode) * (size_t)Lw.scene.n_lds;
-            if (RT_WALK_FIRST && lv == 0) launch_persistent(k_walk_first<4>, st, Lw, mb, lds);
+            if (L.walk_first && lv == 0) launch_persistent(k_walk_first<4>, st, Lw, mb, lds);
             else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb, lds);
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));

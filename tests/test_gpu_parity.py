@@ -281,8 +281,9 @@ def test_cull_equals_exhaustive(ctx, name):
 @pytest.mark.parametrize("name", ["config1", "small3", "small8", "config2"])
 def test_split_equals_fused(ctx, name, monkeypatch):
     """The walk pass + test pass (candidate lists) changes scheduling, not results: identical
-    frames against the fused kernel (RT_CREATE_NO_SPLIT), also when every list overflows
-    (RT_CAND_CAP=1: overflowing pixels re-walk from scratch)."""
+    frames against the fused kernel (RT_CREATE_NO_SPLIT), with level 0 as one walk + first-hit
+    kernel (the default for these scenes) or as two passes (RT_WF_LIST=-1), and when every list
+    overflows (RT_CAND_CAP=1: overflowing pixels re-walk from scratch)."""
     spec = {"config1": scenes.config1_spheres, "small3": lambda: scenes.small_random(3),
             "small8": lambda: scenes.small_random(8, n_tri=800, half=0.04),
             "config2": scenes.config2}[name]()
@@ -296,6 +297,12 @@ def test_split_equals_fused(ctx, name, monkeypatch):
         ctxs.append(fused)
         fused.upload(scene)
         _same_frames(split, fused.trace_frame(cam, cfg, stats=False, allow_fault=True))
+        monkeypatch.setenv("RT_WF_LIST", "-1")        # level 0 as separate walk and first-hit passes
+        sep = rtamd.Context(0)
+        ctxs.append(sep)
+        sep.upload(scene)
+        _same_frames(split, sep.trace_frame(cam, cfg, stats=False, allow_fault=True))
+        monkeypatch.delenv("RT_WF_LIST")
         monkeypatch.setenv("RT_CAND_CAP", "1")
         tiny = rtamd.Context(0)
         ctxs.append(tiny)

@@ -254,3 +254,42 @@ def test_device_restored_after_calls():
         assert torch.cuda.current_device() == 0
     finally:
         m.close()
+
+
+def _n_gpus():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif("_n_gpus() < 2", reason="needs two distinct GPUs (the parity box has one)")
+@pytest.mark.parametrize("gather", ["peer", "rccl"])
+def test_distinct_gpus_equal_single_device(small3, single, gather, monkeypatch):
+    """devices=[0, 1]: the distinct-GPU path (peer access or a two-rank RCCL communicator, cross-device
+    event ordering) gives the one-device frame, the blend and the reference's partial frame after a
+    throw.  Runs only where hipGetDeviceCount() >= 2; the one-GPU box skips it (README)."""
+    spec, scene = small3
+    monkeypatch.setenv("RT_GATHER", gather)
+    cam, cfg = scenes.make_camera(160, 120), scenes.make_config(3)
+    m = _ctx(scene, devices=[0, 1], stripe_rows=8)
+    try:
+        assert m.info()["gather"] == gather and m.info()["n_devices"] == 2
+        _same(single.trace_frame(cam, cfg, allow_fault=True), m.trace_frame(cam, cfg, allow_fault=True))
+        bcfg = scenes.make_config(3, col_weight=0.25)
+        old = np.random.default_rng(2).uniform(0, 2, 160 * 120 * 3).astype(np.float32)
+        _same(single.trace_frame(cam, bcfg, rgb=old.copy(), allow_fault=True),
+              m.trace_frame(cam, bcfg, rgb=old.copy(), allow_fault=True))
+    finally:
+        m.close()
+    tspec = _throwing_scene()
+    tcam, tcfg = scenes.make_camera(96, 72), scenes.make_config(5, default_substance=-1, col_weight=0.5)
+    old = np.random.default_rng(5).random(96 * 72 * 3, dtype=np.float32)
+    tscene = rtamd.build_scene(tspec)
+    a, b = _ctx(tscene, device=0), _ctx(tscene, devices=[0, 1], stripe_rows=3)
+    try:
+        ra = a.trace_frame(tcam, tcfg, rgb=old.copy(), allow_fault=True)
+        rb = b.trace_frame(tcam, tcfg, rgb=old.copy(), allow_fault=True)
+        assert ra["rc"] == rb["rc"] == abi.RT_E_FAULT
+        _same(ra, rb)
+    finally:
+        a.close()
+        b.close()
