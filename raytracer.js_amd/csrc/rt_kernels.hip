@@ -2115,137 +2115,6 @@ __device__ __forceinline__ void first_item(const RtLaunch &L, const RtDevScene &
     first_finish(L, src, cn, res, fault);
 }
 
-// The first-hit pass by whole waves (RT_FIRST_COOP).  A wave's rays have lists of
-// very different lengths (config 5's bounce levels: 64 unrelated rays; a narrow level: fewer rays
-// than lanes), so one lane per ray leaves most lanes idle behind the longest list.  Here the wave's
-// candidates — (ray, k) for k below each ray's list length, ray-major — are cut into 64 equal
-// contiguous chunks, one per lane.  A lane runs its chunk in order with scan_first's single loop;
-// a candidate with an exact hit records (k, slot) in the ray's LDS word by atomic minimum, and the
-// rest of that ray in the chunk is dropped, as is any candidate of a ray whose word already holds a
-// smaller k when the lane reaches it.  Every candidate below a ray's first hit is tested (each lies in
-// exactly one chunk and is dropped only behind a hit), so the minimum k with a hit is the first hit
-// in walk order and its slot the node's minimum-rank hit (node_first_hit): the same result as the
-// ray's own scan.  A ray that cannot be culled tests every prim of each node, as node_first_hit's
-// exhaustive scan does.  Every lane of the wave calls this together (src.valid false: no ray).
-#ifndef RT_FIRST_COOP
-#define RT_FIRST_COOP 0                // measured 6x slower; kept in history only
-#endif
-#ifndef RT_WF_COOP
-#define RT_WF_COOP 0                   // the same in k_walk_first, behind the walk
-#endif
-struct CoopLds {
-    double o[3][256], d[3][256];
-    uint32_t id[256];
-    int32_t n[256];
-    unsigned long long best[256];            // (k << 32) | slot of the ray's first hit so far
-};
-
-__device__ __forceinline__ int wave_incl_scan(int v)
-{
-    const int lane = __lane_id();
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int u = __shfl_up(v, off, 64);
-        if (lane >= off) v += u;
-    }
-    return v;
-}
-
-// LDS operations of one wave complete in order; this keeps the compiler from moving them across
-__device__ __forceinline__ void wave_lds_order()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ int2 first_wave(const RtLaunch &L, const RtDevScene &S, const RaySrc &src, int cn,
-                                           uint32_t stride, bool fault, Counters &c)
-{
-    __shared__ CoopLds sh;
-    const int lane = __lane_id();
-    const int wb = threadIdx.x & ~63, me = wb + lane;
-    const bool scan = src.valid && cn >= 4 && !fault;
-    const int n = scan ? cn >> 2 : 0;
-    sh.n[me] = n;
-    sh.best[me] = ~0ull;
-    if (scan) {
-        for (int i = 0; i < 3; i++) { sh.o[i][me] = src.o[i]; sh.d[i][me] = src.d[i]; }
-        sh.id[me] = (uint32_t)src.id;
-    }
-    const int P = wave_incl_scan(n);                         // candidates of rays 0..lane
-    const int T = __shfl(P, 63, 64);
-    wave_lds_order();
-    if (T > 0) {
-        const int b = (T * lane) >> 6, e = (T * (lane + 1)) >> 6;   // this lane's chunk [b, e)
-        int r = 0;                                           // the ray of candidate b: #rays with P <= b
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-            const int pv = __shfl(P, r + step - 1, 64);
-            if (pv <= b) r += step;
-        }
-        int kb = __shfl(P - n, r & 63, 64);                  // candidates before ray r
-        int t = b, nr = t < e ? sh.n[wb + r] : 0, k = 0, i = -1, slot = 0, prim_end = 0;
-        int best_rank = 0x7fffffff, best_slot = -1;
-        uint32_t rid = 0;
-        bool have = false, busy = false, cull = false;
-        double o[3] = {0, 0, 0}, d[3] = {0, 0, 0};
-        RayBox rb{};
-        while (busy || t < e) {
-            if (busy) {
-                if (slot < prim_end) {
-                    const int rk = S.prim[slot].rank;
-                    if (rk < best_rank) {
-                        Hit h;
-                        c.exact++;
-                        if (prim_hit(S.prim[slot], o, d, h)) { best_rank = rk; best_slot = slot; }
-                    }
-                    slot++;
-                } else if (i >= 0) {
-                    const RtBvh bx = S.bvh[i];
-                    if (!ray_box(bx, rb)) i = bx.skip;
-                    else if (bx.info < 0) i++;
-                    else { slot = bx.info >> 4; prim_end = slot + (bx.info & 15); i = bx.skip; }
-                } else {
-                    if (best_slot >= 0) {                    // this candidate hits: the ray is done here
-                        atomicMin(&sh.best[wb + r], ((unsigned long long)k << 32) | (uint32_t)best_slot);
-                        t = t > kb + nr ? t : kb + nr;
-                    }
-                    busy = false;
-                }
-            } else {
-                while (t >= kb + nr) { kb += nr; r++; nr = sh.n[wb + r]; have = false; }
-                k = t - kb;
-                if (sh.best[wb + r] < ((unsigned long long)k << 32)) { t = kb + nr; continue; }   // hit earlier
-                if (!have) {
-                    for (int a = 0; a < 3; a++) { o[a] = sh.o[a][wb + r]; d[a] = sh.d[a][wb + r]; }
-                    rid = sh.id[wb + r];
-                    rb = make_raybox(o, d);
-                    cull = L.cull != 0 && rb.ok;
-                    have = true;
-                }
-                const int node = cand_load(L, k, stride, rid);
-                const int4 hdr = ld_node<int4>(S, node, NODE_NENT);      // {n_ent, ent_begin, bvh_root, -}
-                i = -1;
-                slot = prim_end = 0;
-                // as scan_first / node_first_hit: the root's children, or a leaf root's prims; a ray
-                // that cannot be culled tests every prim of the node (the rank rule makes the order moot)
-                if (!cull || (RT_EMIT_BOX && hdr.x <= S.bvh_leaf)) { slot = hdr.y; prim_end = hdr.y + hdr.x; }
-                else i = RT_EMIT_BOX ? hdr.z + 1 : hdr.z;
-                best_rank = 0x7fffffff;
-                best_slot = -1;
-                busy = true;
-                t++;
-            }
-        }
-    }
-    wave_lds_order();
-    int2 res = make_int2(-1, -1);
-    const unsigned long long bst = sh.best[me];
-    if (scan && bst != ~0ull) res = make_int2(cand_load(L, (int)(bst >> 32), stride, (uint32_t)src.id), (int)(uint32_t)bst);
-    return res;
-}
-
 // After the scan: at level 0 the plain terminal rays end here (early_shade) and the others are queued
 // for k_shade; first[id] = {node, slot} or {-1, -1}.
 __device__ __forceinline__ void first_finish(const RtLaunch &L, const RaySrc &src, int cn, int2 res, bool fault)
@@ -2280,15 +2149,8 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
         for (int t = t0; t < t_end; t++) {
             RaySrc src;
             ray_src(L, t, lane, src);
-#if RT_FIRST_COOP
-            const int cn = src.valid ? L.cand_n[src.id] : -1;
-            const int2 res = first_wave(L, S, src, cn, (uint32_t)stride, fault, c);
-            ray_src(L, t, lane, src);                    // again: not kept live across the scan
-            if (src.valid) first_finish(L, src, cn, res, fault);
-#else
             if (!src.valid) continue;
             first_item(L, S, src, L.cand_n[src.id], (uint32_t)stride, fault, c);
-#endif
         }
     }
 }
@@ -2313,16 +2175,9 @@ __global__ void __launch_bounds__(256, MINW) k_walk_first(RtLaunch L)
         if (t >= items) break;
         RaySrc src;
         ray_src(L, t, lane, src);
-#if RT_WF_COOP
-        const int cn = src.valid ? walk_item(L, S, F, src, stride, c) : -1;
-        const int2 res = first_wave(L, S, src, cn, (uint32_t)stride, F.fault != 0, c);
-        ray_src(L, t, lane, src);
-        if (src.valid) first_finish(L, src, cn, res, F.fault != 0);
-#else
         if (!src.valid) continue;
         const int cn = walk_item(L, S, F, src, stride, c);
         first_item<false>(L, S, src, cn, (uint32_t)stride, F.fault != 0, c);
-#endif
     }
 }
 
