@@ -13,7 +13,8 @@ How N GPUs run:
     frame, traces every part on its GPU and gathers on GPU 0 with RCCL inside librt.  Fails (exit 2)
     when fewer than N GPUs exist.
 
-Frames in flight (--inflight P, default 16; 4 for the one-process multi-GPU mode): P contexts, each
+Frames in flight (--inflight P, default 16, or 2 for parts of more than 2^22 pixels; 4 for the
+one-process multi-GPU mode): P contexts, each
 on its own HIP stream with its own frame buffers; frame f runs on context f % P.  HIP maps streams
 onto GPU_MAX_HW_QUEUES hardware queues (HIP's default is 4); the bench raises it to 16 before the
 HIP runtime starts.  A frame's bounce level is a latency-bound tail (few, long continuation rays;
@@ -604,6 +605,13 @@ def fail(msg):
 
 
 # ---- one process per GPU (torchrun) or a single GPU -----------------------------------------------------
+def default_inflight(pixels):
+    """Frames in flight per GPU: 16, or 2 for parts of more than 2^22 pixels.  A 2160p frame fills
+    the GPU on its own; more frames in flight only share the caches (config 5: 303 Mrays/s at 16,
+    313 at 2; config 4: 1081 at 16, 1084 serial; profiles/r3_v22/)."""
+    return 2 if pixels > (1 << 22) else 16
+
+
 def run_ranks(args, spec, scene, W, H, refmax, world, rank, local):
     if os.environ.get("RT_BENCH_BACKEND") == "gloo":
         local %= torch.cuda.device_count()       # plumbing check: ranks may share the box's one GPU
@@ -616,7 +624,7 @@ def run_ranks(args, spec, scene, W, H, refmax, world, rank, local):
                                 **({"device_id": dev} if backend == "nccl" else {}))
         if dist.get_world_size() != args.gpus:
             fail("torch.distributed world size %d != --gpus %d" % (dist.get_world_size(), args.gpus))
-    P = max(1, min(args.inflight or 16, args.steps))
+    P = max(1, min(args.inflight or default_inflight(W * H // max(1, world)), args.steps))
     ctxs = []
     for _ in range(P):
         c = rtamd.Context(local)
