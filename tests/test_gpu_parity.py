@@ -313,6 +313,29 @@ def test_split_equals_fused(ctx, name, monkeypatch):
             c.close()
 
 
+@pytest.mark.parametrize("leaf", ["2", "5"])
+def test_bvh_leaf_sizes_equal_default(ctx, leaf, monkeypatch):
+    """Cull-hierarchy leaves of several entities (RT_BVH_LEAF; the first-hit scans test a leaf's prims
+    one per trip) change work, not results: split and fused frames equal the default
+    (leaf 1) frame, at refmax 5 with mirrors and lights."""
+    spec = scenes.small_random(8, n_tri=800, half=0.04)
+    cam, cfg = scenes.make_camera(256, 160), scenes.make_config(5)
+    scene = rtamd.build_scene(spec)
+    ctx.upload(scene)
+    want = ctx.trace_frame(cam, cfg, stats=False, allow_fault=True)
+    monkeypatch.setenv("RT_BVH_LEAF", leaf)
+    ctxs = []
+    try:
+        for flags in (0, abi.RT_CREATE_NO_SPLIT):
+            c = rtamd.Context(0, flags=flags)
+            ctxs.append(c)
+            c.upload(scene)
+            _same_frames(want, c.trace_frame(cam, cfg, stats=False, allow_fault=True))
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 @pytest.mark.parametrize("group", ["1", "3", "16", "48", "64"])
 def test_continuation_rays_per_wave(ctx, group, monkeypatch):
     """Bounce levels take RT_CONT_GROUP rays per wave, up to 64 when a level is large (cont_g:
