@@ -110,6 +110,7 @@ struct rt_ctx {
                                      // slowest wave
     int seg = 8;                     // segments per bounce ray, levels >= 1 (RT_SEG: 0/1 off, 2..64)
     int lv_blocks = 0;               // grid cap of bounce-level passes (RT_LV_BLOCKS; 0: persistent occupancy)
+    int l0_blocks = 0;               // grid cap of the level-0 passes (RT_L0_BLOCKS; 0: persistent occupancy)
     int refill = 16;                 // wide bounce levels walked with per-lane refill (RT_REFILL; 0: off)
     bool refill_always = false;      // RT_REFILL_ALWAYS=1: also levels no recent frame showed wide (tests)
     int seg_max = 64 * 4096;         // bounce levels of more rays run unsegmented, refilled (RT_SEG_MAX; 0: no limit)
@@ -225,6 +226,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_CONT_GROUP")) c->cont_group = pow2_at_most_64(atoi(e));
     if (const char *e = getenv("RT_SEG")) c->seg = atoi(e) > 1 ? pow2_at_most_64(atoi(e)) : 0;
     if (const char *e = getenv("RT_LV_BLOCKS")) c->lv_blocks = atoi(e) < 0 ? 0 : atoi(e);
+    if (const char *e = getenv("RT_L0_BLOCKS")) c->l0_blocks = atoi(e) < 0 ? 0 : atoi(e);
     if (const char *e = getenv("RT_REFILL")) c->refill = atoi(e) < 0 ? 0 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_REFILL_ALWAYS")) c->refill_always = atoi(e) != 0;
     if (const char *e = getenv("RT_SEG_MAX")) c->seg_max = atoi(e) < 0 ? 0 : atoi(e);
@@ -554,13 +556,17 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
                 }
             }
         (void)hipGetLastError();                                            // hipErrorNotReady
-        // this frame's copy goes to a buffer without a transfer in flight, else to the older one
-        const int w = !d.ctr_pend[0] ? 0 : (!d.ctr_pend[1] ? 1 : (d.ctr_seq[0] < d.ctr_seq[1] ? 0 : 1));
-        d.ctr_pend[w] = true;
-        d.ctr_seq[w] = ++d.ctr_frames;
+        // this frame's counters go to a buffer without a transfer in flight; with both busy (frames in
+        // flight) the frame sends none: any recent frame's counts will do for the hints, and a small
+        // part's frame then no longer pays a copy per frame
         L.ctr_hint = d.ctr_snap.data();
-        L.ctr_out = d.h_ctr + (size_t)w * RT_CTR_INTS;
-        L.ctr_done = d.ctr_ev[w];
+        if (!d.ctr_pend[0] || !d.ctr_pend[1]) {
+            const int w = !d.ctr_pend[0] ? 0 : 1;
+            d.ctr_pend[w] = true;
+            d.ctr_seq[w] = ++d.ctr_frames;
+            L.ctr_out = d.h_ctr + (size_t)w * RT_CTR_INTS;
+            L.ctr_done = d.ctr_ev[w];
+        }
     }
     L.occ = c->occ;
     L.diag = c->diag;
@@ -571,6 +577,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.shade_occ = c->shade_occ;
     L.seg = c->seg;
     L.lv_blocks = c->lv_blocks;
+    L.l0_blocks = c->l0_blocks;
     L.refill = c->refill;
     L.refill_always = c->refill_always;
     L.seg_max = c->seg_max;
@@ -1077,7 +1084,7 @@ extern "C" int rt_trace_rows_device(rt_ctx *c, const rt_camera_desc *cam, const 
     hipStream_t st = stream ? (hipStream_t)stream : d0.stream;
     L.rgb = (float *)d_rgb;
     if ((r = bridge_in(d0, st)) != RT_OK) return r;
-    HIP_TRY(hipMemsetAsync(d0.b_fault.p, 0, sizeof(int), st));
+    L.zero_fault = 1;                            // k_frame_start clears the fault flag (one launch per frame)
     if (stats) {
         HIP_TRY(hipMemsetAsync(d0.b_counters.p, 0, sizeof(unsigned long long) * CT_N, st));
         L.counters = (unsigned long long *)d0.b_counters.p;

@@ -180,6 +180,7 @@ struct RtLaunch {
     uint8_t *status;                            // device [rows*W] or null
     unsigned long long *counters;               // device [CT_N] or null (stats build)
     int32_t *fault;                             // device flag: some ray hit a reference throw
+    int32_t zero_fault;                         // k_frame_start clears *fault (callers with one launch per frame)
     int32_t blend;                              // col_weight != 1: read-modify-write rgb
     int32_t skip_trace;                         // ray generation only (rt_debug_camera_dirs)
     int32_t cull;                               // use the per-node cull hierarchies
@@ -202,6 +203,7 @@ struct RtLaunch {
     int32_t seg;                                // segments per bounce ray, levels >= 1 (0: off; RT_SEG; §5.10)
     int32_t *ray_cn;                            // device [rows*W]: per-ray status of a segmented level
     int32_t lv_blocks;                          // grid cap of the bounce-level passes and k_cont (0: full; RT_LV_BLOCKS)
+    int32_t l0_blocks;                          // grid cap of the level-0 passes (0: full; RT_L0_BLOCKS)
     int32_t refill;                             // wide bounce levels: idle lanes that take new rays (0: off; RT_REFILL)
     int32_t refill_always;                      // refill every wide level, not only where a recent frame had one (tests)
     int32_t seg_max;                            // bounce levels of more rays run unsegmented (0: no limit; RT_SEG_MAX)

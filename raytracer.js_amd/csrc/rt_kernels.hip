@@ -1140,10 +1140,16 @@ __device__ __forceinline__ void rotate_1(double &x, double &y, double c, double 
 
 __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
                                                      RtFrameSetup *setup, int part, int n_parts, int stripe,
-                                                     int rows, int row0, double *__restrict__ dirs)
+                                                     int rows, int row0, double *__restrict__ dirs, int32_t *ctr,
+                                                     int32_t *fault)
 {
     const int lane = threadIdx.x & 63;
     if (blockIdx.x == 0) {
+        // the frame's work counters (and, when asked, its fault flag) start at zero: the frame's later
+        // kernels follow in stream order
+        if (ctr)
+            for (int i = threadIdx.x; i < RT_CTR_INTS; i += blockDim.x) ctr[i] = 0;
+        if (fault && threadIdx.x == 0) *fault = 0;
         if (threadIdx.x >= 64) return;
         long long lv = 0;
         int t = -1, oc = 0;
@@ -2328,6 +2334,9 @@ static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const Rt
     hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, st, L);
 }
 
+#ifndef RT_NO_OP_BLOCKS
+#define RT_NO_OP_BLOCKS 8              // grid of a bounce-level kernel predicted to return at once (0: full)
+#endif
 // Grid of a bounce-level pass (or k_cont).  Persistent passes are correct at any grid size: waves
 // claim work until the level's queue is empty.  A level of a small part holds a few thousand rays,
 // and launching the full persistent grid for it costs more in block dispatch than the work (8-part
@@ -2349,16 +2358,17 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     const int W = L.cam.width;
     const int rg_lanes = 6 * (L.rows > 0 ? L.rows : 0);
     (void)hipGetLastError();                     // a stale error of an earlier runtime call is not ours
+    const bool trace = L.rows > 0 && !L.skip_trace;
     hipLaunchKernelGGL(k_frame_start, dim3(1 + (rg_lanes + 255) / 256), dim3(256), 0, st, L.scene, L.cam, L.cfg,
-                       L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.row0, L.dirs);
+                       L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.row0, L.dirs, trace ? L.ctr : nullptr,
+                       L.zero_fault ? L.fault : nullptr);
     HIP_TRY(hipGetLastError());
-    if (L.rows <= 0 || L.skip_trace) {           // an empty part (more devices than stripes): no trace
+    if (!trace) {                                // an empty part (more devices than stripes): no trace
         if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
         if (ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
         return RT_OK;
     }
     (void)W;
-    HIP_TRY(hipMemsetAsync(L.ctr, 0, sizeof(int32_t) * RT_CTR_INTS, st));
     if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
     // occupancy variants (waves per SIMD the register allocation must admit); RT_OCC selects
     if (L.counters) {
@@ -2379,23 +2389,42 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             Lv.level = lv;
             Lv.last_level = lv == levels && levels < want;
             const int32_t hint = lv >= 1 && L.ctr_hint ? L.ctr_hint[4 + RT_CTR_LEVEL * (lv - 1)] : -1;
-            const int mb = lv >= 1 ? level_blocks(L, hint) : 0;
+            const int mb = lv >= 1 ? level_blocks(L, hint) : L.l0_blocks;
             // per-lane refill only where a recent frame had a wide level (both walk kernels read Lv.refill)
             Lv.refill = L.refill_always || hint > 64 * 4096 ? L.refill : 0;
+            // A bounce level runs either segmented (k_walk_seg, k_first_seg), refilled (k_walk_refill,
+            // k_first) or plain (k_walk, k_first); the kernels decide from the level's ray count on the
+            // device, and the others return at once.  With a recent count (hint) the host predicts the
+            // mode as seg_mode / refill_level do and launches the kernels that will return with
+            // NO_OP_BLOCKS blocks: a persistent pass is correct at any grid, so a wrong prediction only
+            // costs time, and a small part's frame no longer dispatches full grids that do nothing.
+            int mb_plain = mb, mb_seg = mb, mb_refill = mb, mb_first = mb, mb_first_seg = mb;
+            if (lv >= 1 && hint >= 0 && RT_NO_OP_BLOCKS > 0) {
+                const long long P = (long long)L.rows * (long long)L.cam.width;
+                const bool seg = L.seg > 1 && (L.seg_max <= 0 || hint <= L.seg_max) && (long long)hint * L.seg <= P;
+                int g = L.cont_group;
+                while (g < 64 && (long long)g * 4096 < (long long)hint) g *= 2;
+                const bool refill = !seg && Lv.refill > 0 && g >= 64;
+                if (seg) mb_plain = mb_refill = mb_first = RT_NO_OP_BLOCKS;
+                else mb_seg = mb_first_seg = RT_NO_OP_BLOCKS;
+                if (refill) mb_plain = RT_NO_OP_BLOCKS;
+                else mb_refill = RT_NO_OP_BLOCKS;
+            }
             if (lv == 0 && walk_wait) HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)walk_wait, 0));
             RtLaunch Lw = Lv;                         // the walk kernels read the upper levels from LDS
             Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
             const size_t lds = sizeof(RtNode) * (size_t)Lw.scene.n_lds;
             if (L.walk_first && lv == 0) launch_persistent(k_walk_first<4>, st, Lw, mb, lds);
-            else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb, lds);
+            else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb_plain, lds);
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
-            if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lw, mb, lds);   // one of the two runs (§5.10)
-            if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<RT_REFILL_OCC>, st, Lw, mb, lds);
-            launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv, mb);
+            if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lw, mb_seg, lds);   // one of the two runs (§5.10)
+            if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<RT_REFILL_OCC>, st, Lw, mb_refill, lds);
+            if (!(L.walk_first && lv == 0))              // k_walk_first took level 0's first-hit pass
+                launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv, mb_first);
             HIP_TRY(hipGetLastError());
             if (RT_FIRST_REFILL && lv >= 1 && Lv.refill > 0) launch_persistent(k_first_refill<6>, st, Lv, mb);
-            if (lv >= 1 && L.seg > 1) launch_persistent(k_first_seg<4>, st, Lv, mb);
+            if (lv >= 1 && L.seg > 1) launch_persistent(k_first_seg<4>, st, Lv, mb_first_seg);
             launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
         }

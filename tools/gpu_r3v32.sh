@@ -1,0 +1,12 @@
+set -u
+OUT=gpurun_out/r3v32
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1 || exit $?
+timeout -k 10 200 python tools/pipeline_probe.py --config config3 --parts 1 2 4 8 --inflight 1 16 --frames 64 > $OUT/probe_new.log 2>&1 || exit $?
+RT_LIB=$PWD/raytracer.js_amd/lib/librt_amd_fullgrid.so timeout -k 10 200 python tools/pipeline_probe.py --config config3 --parts 1 2 4 8 --inflight 1 16 --frames 64 > $OUT/probe_fullgrid.log 2>&1 || exit $?
+timeout -k 10 200 python tools/pipeline_probe.py --config config3 --parts 1 2 4 8 --inflight 1 16 --frames 64 > $OUT/probe_new2.log 2>&1 || exit $?
+T0=$(date +%s)
+timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 --profile-out $OUT/prof3 > $OUT/bench.log 2>&1 || exit $?
+echo "command: python3 bench.py --gpus 1 --steps 20 --warmup 5 --profile-out $OUT/prof3; wall $(( $(date +%s) - T0 )) s" > $OUT/driver_cmd_wall.txt
+timeout -k 10 400 python3 bench.py --config config5 --no-js --cpu-budget 0 --profile-out $OUT/prof5 > $OUT/bench_config5.log 2>&1 || exit $?

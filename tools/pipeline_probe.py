@@ -53,10 +53,12 @@ def main():
             t0 = time.perf_counter()
             for i in range(a.frames):
                 ctxs[i % p].trace_rows_device(cam, cfg, 0, parts, 8, bufs[i % p].data_ptr(), streams[i % p].cuda_stream)
+            t_sub = time.perf_counter() - t0                 # host time to submit (launches return early)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / a.frames
             print(json.dumps(dict(parts=parts, inflight=p, ms_per_frame=round(dt * 1e3, 3),
-                                  mrays_per_gpu=round(seg / dt / 1e6, 1))), flush=True)
+                                  mrays_per_gpu=round(seg / dt / 1e6, 1),
+                                  host_submit_ms_per_frame=round(t_sub / a.frames * 1e3, 3))), flush=True)
     for c in ctxs:
         c.close()
 
