@@ -64,3 +64,25 @@ def test_usable_cores_reports_quota():
     n, visible, quota = bench.usable_cores()
     assert 1 <= n <= visible
     assert quota is None or n <= quota
+
+
+def test_fused_level0_pools_walk_and_first_bytes():
+    """With k_walk_first in the trace the walk and first-hit passes' algorithmic bytes
+    are one pool, shared by every walk / first-hit kernel in proportion to its time."""
+    import bench
+    dur = {"k_walk_first": 3.0, "k_walk_seg": 0.5, "k_first_seg": 0.5}
+    counters = dict(n_ret=10, n_slot=20, n_loc=30, n_cull=40, n_exact=50, n_hit=60, segments=70, primary=7)
+    kr = bench.kernel_rooflines(dur, {}, counters)
+    pool = 48 * 10 + 32 * 20 + 40 * 30 + 32 * 40 + 80 * 50
+    got = sum(kr[k]["alg_bytes_cache_served"] for k in dur)
+    assert got == pytest.approx(pool, abs=3)
+    assert kr["k_walk_first"]["alg_bytes_cache_served"] == pytest.approx(pool * 3.0 / 4.0, abs=2)
+
+
+def test_default_frames_in_flight():
+    """16 frames in flight, 2 for parts of more than 2^22 pixels (a 2160p part fills the GPU alone)."""
+    import bench
+    assert bench.default_inflight(1920 * 1080) == 16
+    assert bench.default_inflight(3840 * 2160) == 2
+    assert bench.default_inflight(3840 * 2160 // 2) == 16
+    assert bench.default_inflight(1 << 22) == 16
