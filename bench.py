@@ -90,8 +90,8 @@ BYTES_KERNEL = dict(n_ret=48, n_slot=32, n_loc=40, n_cull=32, n_exact=80, n_hit=
 BYTES_REF = dict(n_ret=48, n_slot=32, n_loc=40, n_sph=36, n_box=36, n_tri=76, n_hit=40, primary=12)
 KERNEL_PASS = {"k_walk": "walk", "k_walk_seg": "walk", "k_walk_refill": "walk", "k_first": "first",
                "k_first_seg": "first", "k_first_refill": "first", "k_shade": "shade"}
-TRACE_KERNELS = ("k_walk_first", "k_walk", "k_walk_seg", "k_walk_refill", "k_first", "k_first_seg", "k_first_refill",
-                 "k_shade", "k_cont", "k_trace", "k_frame_start")
+TRACE_KERNELS = ("k_walk_first", "k_seg", "k_walk", "k_walk_seg", "k_walk_refill", "k_first", "k_first_seg",
+                 "k_first_refill", "k_shade", "k_cont", "k_trace", "k_frame_start")
 PMC_FRAMES = 4                 # frames the --pmc-child run profiles (after one warm-up frame)
 PMC_PASSES = {
     "fetch": ["FETCH_SIZE"],
@@ -440,12 +440,13 @@ def kernel_rooflines(dur, pmc, counters):
     SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU of 64; HBM: 2*FETCH_SIZE + WRITE_SIZE (KiB; FETCH_SIZE
     doubled on gfx950) over the duration against 8 TB/s; algorithmic bytes (§8(d), cache-served)."""
     out = {}
-    # level 0 as one walk + first-hit kernel (k_walk_first, DESIGN.md §5.18): the walk and first-hit
-    # passes' algorithmic bytes are one pool, shared by their kernels in proportion to time
+    # walk and first-hit passes fused into one kernel (k_walk_first at level 0, DESIGN.md §5.18; k_seg
+    # on segmented levels, §5.10): the two passes' algorithmic bytes are one pool, shared by their
+    # kernels in proportion to time
     pass_of, pass_bytes = dict(KERNEL_PASS), dict(PASS_BYTES)
-    if "k_walk_first" in dur:
+    if "k_walk_first" in dur or "k_seg" in dur:
         pass_of = {k: ("walk+first" if p in ("walk", "first") else p) for k, p in pass_of.items()}
-        pass_of["k_walk_first"] = "walk+first"
+        pass_of["k_walk_first"] = pass_of["k_seg"] = "walk+first"
         pass_bytes["walk+first"] = dict(PASS_BYTES["walk"], **PASS_BYTES["first"])
     for k, ms in sorted(dur.items(), key=lambda kv: -kv[1]):
         c = pmc.get(k, {})

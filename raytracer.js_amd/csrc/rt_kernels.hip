@@ -1733,10 +1733,134 @@ __device__ __forceinline__ bool seg_mode(const RtLaunch &L)
            (long long)n * L.seg <= (long long)L.rows * (long long)L.cam.width;
 }
 
-// Walk pass, segmented: K = L.seg lanes per ray, lane = (ray lane / K, segment lane % K);
-// per-segment lists at index ray * K + segment, cand_n = count * 8 + SEG_* (or -1 on overflow).
+// Segmented bounce levels: K = L.seg lanes per ray, lane = (ray lane / K,
+// segment lane % K), 64 / K rays per work item; per-segment lists at index ray * K + segment.
+struct SegLane {
+    int K, rpw, j, base, n_rays;
+    double frac;
+};
+__device__ __forceinline__ SegLane seg_lane(const RtLaunch &L)
+{
+    SegLane g;
+    const int lane = threadIdx.x & 63;
+    g.K = L.seg;
+    g.rpw = 64 / g.K;                            // rays per wave
+    g.j = lane & (g.K - 1);
+    g.base = lane & ~(g.K - 1);
+    g.n_rays = *lvl_ctr(L, L.level - 1);
+    g.frac = (double)g.j / (double)g.K;
+    return g;
+}
+
+// The walk of work item t's segments: returns this lane's cand_n = count * 8 + SEG_* (or -1 on
+// overflow; SEG_SKIP without a ray) and stores it.
+__device__ __forceinline__ int seg_walk_item(const RtLaunch &L, const RtDevScene &S, const SegLane &g, int t,
+                                             size_t stride, Counters &c)
+{
+    const int lane = threadIdx.x & 63;
+    const int K = g.K, j = g.j, base = g.base;
+    const int q = t * g.rpw + lane / K;
+    const bool valid = q < g.n_rays;
+    Walker w;
+    int end = SEG_SKIP, seat = -1;
+    if (valid) {
+        const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
+        const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
+        if (j == 0) {
+            end = walker_set(S, w, o, d, false, 0, 0, c) < 0 ? SEG_SEATTHROW : SEG_FIN;
+        } else {
+            const NodeDims r = node_dims(S, 0);
+            BoxIsect bi;
+            if (box_isect(r.x + 0.5 * r.s, r.y + 0.5 * r.s, r.z + 0.5 * r.s, r.s, o, d, bi)) {
+                const double t0 = bi.u1 > 0 ? bi.u1 : 0.0, t1 = bi.u2;
+                if (t1 > t0 && t1 < 1e300) {
+                    const double tt = t0 + (t1 - t0) * g.frac;
+                    const double x[3] = {o[0] + d[0] * tt, o[1] + d[1] * tt, o[2] + d[2] * tt};
+                    int tree = -1, oct = 0;
+                    if (node_at_pos(S, x, tree, oct, c.loc) == 1 && walker_set(S, w, o, d, true, tree, oct, c) >= 0) {
+                        seat = tree * 8 + oct;
+                        end = SEG_FIN;
+                    }
+                }
+            }
+        }
+    }
+    // the stop cell: the seat of the next segment of this ray that has one
+    int stop = -1;
+    for (int k = 1; k < K; k++) {
+        const int s = __shfl(seat, base | (j + k < K ? j + k : K - 1), 64);
+        if (stop < 0 && j + k < K && s >= 0) stop = s;
+    }
+    int n = 0;
+    if (end == SEG_FIN) {
+        const RayBox rb = make_raybox(w.o, w.d);
+        const size_t id = (size_t)q * K + j;
+        auto emit = [&](int node) {
+            if (!node_candidate(S, node, L.cull != 0, rb)) return;
+            if (n < L.cand_cap) cand_store(L, n, (uint32_t)stride, (uint32_t)id, node);
+            n++;
+        };
+        const int r = walker_run<true>(S, w, emit, stop);
+        if (r < 0) end = r == -2 ? SEG_CAP : SEG_THROW;
+        else if (r == 2) end = SEG_REACHED;
+    }
+    const int cn = valid ? (n > L.cand_cap ? -1 : n * 8 + end) : SEG_SKIP;
+    if (valid) L.cand_n[(size_t)q * K + j] = cn;
+    return cn;
+}
+
+// The first-hit scan of work item t's segments, from each lane's cand_n (`cn`, as seg_walk_item
+// returned or stored it): each lane scans its segment's list if every earlier segment of the ray
+// reached its successor; lane 0 of the ray's group then takes the segments in order.  Writes
+// first[ray] and ray_cn[ray] (the unsegmented cand_n convention k_shade reads: -1 overflow, else end
+// status in the low 2 bits).
+__device__ __forceinline__ void seg_first_item(const RtLaunch &L, const RtDevScene &S, const SegLane &g, int t, int cn,
+                                               size_t stride, bool fault, Counters &c)
+{
+    const int lane = threadIdx.x & 63;
+    const int K = g.K, j = g.j, base = g.base;
+    const int q = t * g.rpw + lane / K;
+    const bool valid = q < g.n_rays;
+    const size_t id = (size_t)q * K + j;
+    bool open = true;                   // all earlier segments reached their successor
+    for (int k = 0; k < K - 1; k++) {
+        const int s = __shfl(cn, base | k, 64);
+        if (k < j && !(s >= 0 && ((s & 7) == SEG_REACHED || (s & 7) == SEG_SKIP))) open = false;
+    }
+    int2 res = make_int2(-1, -1);
+    if (valid && open && cn >= 8 && !fault) {
+        const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
+        const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
+        res = scan_first(L, S, o, d, make_raybox(o, d), (uint32_t)stride, (uint32_t)id, cn >> 3, c);
+    }
+    // in segment order: overflow -> the whole ray to k_cont; a hit wins; an end ends the ray
+    bool done = false;
+    int2 out = make_int2(-1, -1);
+    int ocn = 0;
+    for (int k = 0; k < K; k++) {
+        const int s = __shfl(cn, base | k, 64);
+        const int rx = __shfl(res.x, base | k, 64), ry = __shfl(res.y, base | k, 64);
+        if (done) continue;
+        if (s < 0) { done = true; ocn = -1; }
+        else if (ry >= 0) { done = true; out = make_int2(rx, ry); ocn = 4; }
+        else if ((s & 7) != SEG_REACHED && (s & 7) != SEG_SKIP) { done = true; ocn = s & 3; }
+    }
+    if (valid && j == 0) {
+        reinterpret_cast<int2 *>(L.first)[q] = out;
+        L.ray_cn[q] = ocn;
+    }
+}
+
+// RT_SEG_FUSED = 1 (default): a segmented level's walk and first-hit scan run as one pass, k_seg:
+// a wave walks its item's segments and then scans their lists, whose counts it holds in registers,
+// as k_walk_first does for level 0.  These levels are latency-bound (few, long rays), so a second
+// launch cost its own drain and, with frames in flight, a slot among the few kernels the GPU runs at
+// once (small parts).
+#ifndef RT_SEG_FUSED
+#define RT_SEG_FUSED 1
+#endif
 template <int MINW>
-__global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
+__global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
 {
     if (!seg_mode(L)) return;
     stage_top(L.scene);
@@ -1744,116 +1868,54 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
-    const int n_rays = *lvl_ctr(L, L.level - 1);
-    const int K = L.seg, rpw = 64 / K;           // segments per ray, rays per wave
-    const int items = (n_rays + rpw - 1) / rpw;
-    const int j = lane & (K - 1), base = lane & ~(K - 1);
-    const double frac = (double)j / (double)K;
+    const bool fault = L.setup->fault != 0;
+    const SegLane g = seg_lane(L);
+    const int items = (g.n_rays + g.rpw - 1) / g.rpw;
     for (;;) {
         int t_end;
         const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
         if (t >= items) break;
-        const int q = t * rpw + lane / K;
-        const bool valid = q < n_rays;
-        Walker w;
-        int end = SEG_SKIP, seat = -1;
-        if (valid) {
-            const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
-            const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
-            if (j == 0) {
-                end = walker_set(S, w, o, d, false, 0, 0, c) < 0 ? SEG_SEATTHROW : SEG_FIN;
-            } else {
-                const NodeDims r = node_dims(S, 0);
-                BoxIsect bi;
-                if (box_isect(r.x + 0.5 * r.s, r.y + 0.5 * r.s, r.z + 0.5 * r.s, r.s, o, d, bi)) {
-                    const double t0 = bi.u1 > 0 ? bi.u1 : 0.0, t1 = bi.u2;
-                    if (t1 > t0 && t1 < 1e300) {
-                        const double tt = t0 + (t1 - t0) * frac;
-                        const double x[3] = {o[0] + d[0] * tt, o[1] + d[1] * tt, o[2] + d[2] * tt};
-                        int tree = -1, oct = 0;
-                        if (node_at_pos(S, x, tree, oct, c.loc) == 1 && walker_set(S, w, o, d, true, tree, oct, c) >= 0) {
-                            seat = tree * 8 + oct;
-                            end = SEG_FIN;
-                        }
-                    }
-                }
-            }
-        }
-        // the stop cell: the seat of the next segment of this ray that has one
-        int stop = -1;
-        for (int k = 1; k < K; k++) {
-            const int s = __shfl(seat, base | (j + k < K ? j + k : K - 1), 64);
-            if (stop < 0 && j + k < K && s >= 0) stop = s;
-        }
-        int n = 0;
-        if (end == SEG_FIN) {
-            const RayBox rb = make_raybox(w.o, w.d);
-            const size_t id = (size_t)q * K + j;
-            auto emit = [&](int node) {
-                if (!node_candidate(S, node, L.cull != 0, rb)) return;
-                if (n < L.cand_cap) cand_store(L, n, (uint32_t)stride, (uint32_t)id, node);
-                n++;
-            };
-            const int r = walker_run<true>(S, w, emit, stop);
-            if (r < 0) end = r == -2 ? SEG_CAP : SEG_THROW;
-            else if (r == 2) end = SEG_REACHED;
-        }
-        if (valid) L.cand_n[(size_t)q * K + j] = n > L.cand_cap ? -1 : n * 8 + end;
+        const int cn = seg_walk_item(L, S, g, t, stride, c);
+        seg_first_item(L, S, g, t, cn, stride, fault, c);
     }
 }
 
-// First-hit pass, segmented: each lane scans its segment's list if every earlier segment of the
-// ray reached its successor; lane 0 of the ray's group then takes the segments in order.  Writes
-// first[ray] and ray_cn[ray] (the unsegmented cand_n convention k_shade reads: -1 overflow, else
-// end status in the low 2 bits).
+// The two passes apart (RT_SEG_FUSED = 0).
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
+{
+    if (!seg_mode(L)) return;
+    stage_top(L.scene);
+    const int lane = threadIdx.x & 63;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    const SegLane g = seg_lane(L);
+    const int items = (g.n_rays + g.rpw - 1) / g.rpw;
+    for (;;) {
+        int t_end;
+        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
+        if (t >= items) break;
+        seg_walk_item(L, L.scene, g, t, stride, c);
+    }
+}
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
 {
     if (!seg_mode(L)) return;
     const int lane = threadIdx.x & 63;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const bool fault = L.setup->fault != 0;
-    const int n_rays = *lvl_ctr(L, L.level - 1);
-    const int K = L.seg, rpw = 64 / K;
-    const int items = (n_rays + rpw - 1) / rpw;
-    const int j = lane & (K - 1), base = lane & ~(K - 1);
+    const SegLane g = seg_lane(L);
+    const int items = (g.n_rays + g.rpw - 1) / g.rpw;
     for (;;) {
         int t_end;
         const int t = claim_xcd(pass_heads(L, L.level, 2), items, lane, 1, t_end, L.xcd_mask & 2);
         if (t >= items) break;
-        const int q = t * rpw + lane / K;
-        const bool valid = q < n_rays;
-        const size_t id = (size_t)q * K + j;
-        const int cn = valid ? L.cand_n[id] : SEG_SKIP;
-        bool open = true;                   // all earlier segments reached their successor
-        for (int k = 0; k < K - 1; k++) {
-            const int s = __shfl(cn, base | k, 64);
-            if (k < j && !(s >= 0 && ((s & 7) == SEG_REACHED || (s & 7) == SEG_SKIP))) open = false;
-        }
-        int2 res = make_int2(-1, -1);
-        if (valid && open && cn >= 8 && !fault) {
-            const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
-            const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
-            res = scan_first(L, S, o, d, make_raybox(o, d), (uint32_t)stride, (uint32_t)id, cn >> 3, c);
-        }
-        // in segment order: overflow -> the whole ray to k_cont; a hit wins; an end ends the ray
-        bool done = false;
-        int2 out = make_int2(-1, -1);
-        int ocn = 0;
-        for (int k = 0; k < K; k++) {
-            const int s = __shfl(cn, base | k, 64);
-            const int rx = __shfl(res.x, base | k, 64), ry = __shfl(res.y, base | k, 64);
-            if (done) continue;
-            if (s < 0) { done = true; ocn = -1; }
-            else if (ry >= 0) { done = true; out = make_int2(rx, ry); ocn = 4; }
-            else if ((s & 7) != SEG_REACHED && (s & 7) != SEG_SKIP) { done = true; ocn = s & 3; }
-        }
-        if (valid && j == 0) {
-            reinterpret_cast<int2 *>(L.first)[q] = out;
-            L.ray_cn[q] = ocn;
-        }
+        const int q = t * g.rpw + lane / g.K;
+        const int cn = q < g.n_rays ? L.cand_n[(size_t)q * g.K + g.j] : SEG_SKIP;
+        seg_first_item(L, L.scene, g, t, cn, stride, fault, c);
     }
 }
 
@@ -2418,13 +2480,16 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb_plain, lds);
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
-            if (lv >= 1 && L.seg > 1) launch_persistent(k_walk_seg<2>, st, Lw, mb_seg, lds);   // one of the two runs (§5.10)
+            if (lv >= 1 && L.seg > 1) {                 // one of the two runs (§5.10)
+                if (RT_SEG_FUSED) launch_persistent(k_seg<2>, st, Lw, mb_seg, lds);
+                else launch_persistent(k_walk_seg<2>, st, Lw, mb_seg, lds);
+            }
             if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<RT_REFILL_OCC>, st, Lw, mb_refill, lds);
             if (!(L.walk_first && lv == 0))              // k_walk_first took level 0's first-hit pass
                 launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv, mb_first);
             HIP_TRY(hipGetLastError());
             if (RT_FIRST_REFILL && lv >= 1 && Lv.refill > 0) launch_persistent(k_first_refill<6>, st, Lv, mb);
-            if (lv >= 1 && L.seg > 1) launch_persistent(k_first_seg<4>, st, Lv, mb_first_seg);
+            if (lv >= 1 && L.seg > 1 && !RT_SEG_FUSED) launch_persistent(k_first_seg<4>, st, Lv, mb_first_seg);
             launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv, mb);
             HIP_TRY(hipGetLastError());
         }
