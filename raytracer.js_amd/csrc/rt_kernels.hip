@@ -1815,7 +1815,7 @@ __device__ __forceinline__ int seg_walk_item(const RtLaunch &L, const RtDevScene
 // first[ray] and ray_cn[ray] (the unsegmented cand_n convention k_shade reads: -1 overflow, else end
 // status in the low 2 bits).
 __device__ __forceinline__ void seg_first_item(const RtLaunch &L, const RtDevScene &S, const SegLane &g, int t, int cn,
-                                               size_t stride, bool fault, Counters &c)
+                                               size_t stride, bool fault, Counters &c, int2 &out, int &ocn)
 {
     const int lane = threadIdx.x & 63;
     const int K = g.K, j = g.j, base = g.base;
@@ -1835,8 +1835,8 @@ __device__ __forceinline__ void seg_first_item(const RtLaunch &L, const RtDevSce
     }
     // in segment order: overflow -> the whole ray to k_cont; a hit wins; an end ends the ray
     bool done = false;
-    int2 out = make_int2(-1, -1);
-    int ocn = 0;
+    out = make_int2(-1, -1);
+    ocn = 0;
     for (int k = 0; k < K; k++) {
         const int s = __shfl(cn, base | k, 64);
         const int rx = __shfl(res.x, base | k, 64), ry = __shfl(res.y, base | k, 64);
@@ -1859,6 +1859,11 @@ __device__ __forceinline__ void seg_first_item(const RtLaunch &L, const RtDevSce
 #ifndef RT_SEG_FUSED
 #define RT_SEG_FUSED 1
 #endif
+#ifndef RT_SEG_SHADE
+#define RT_SEG_SHADE 0                 // k_seg also shades its level (k_shade skips the level)
+#endif
+__device__ __forceinline__ void shade_ray(const RtLaunch &L, const RtFrameSetup &F, const RayQueues &Q, const RaySrc &src,
+                                          int cn, int2 fh, Counters &c);
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
 {
@@ -1869,6 +1874,8 @@ __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const bool fault = L.setup->fault != 0;
+    const RtFrameSetup F = *L.setup;
+    const RayQueues Q = {L.queue[L.level & 1], lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
     const SegLane g = seg_lane(L);
     const int items = (g.n_rays + g.rpw - 1) / g.rpw;
     for (;;) {
@@ -1876,7 +1883,22 @@ __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
         const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
         if (t >= items) break;
         const int cn = seg_walk_item(L, S, g, t, stride, c);
-        seg_first_item(L, S, g, t, cn, stride, fault, c);
+        int2 out;
+        int ocn;
+        seg_first_item(L, S, g, t, cn, stride, fault, c, out, ocn);
+        if (RT_SEG_SHADE) {
+            // the ray's shading, by the lane of its segment 0 (k_shade's work for this ray)
+            const int q = t * g.rpw + lane / g.K;
+            if (q < g.n_rays && g.j == 0) {
+                RaySrc src;
+                src.valid = true;
+                src.id = (size_t)q;
+                src.rec = L.queue[(L.level - 1) & 1] + q;
+                src.pix = src.rec->pix;
+                for (int i = 0; i < 3; i++) { src.o[i] = src.rec->o[i]; src.d[i] = src.rec->d[i]; }
+                shade_ray(L, F, Q, src, ocn, out, c);
+            }
+        }
     }
 }
 
@@ -1915,7 +1937,9 @@ __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
         if (t >= items) break;
         const int q = t * g.rpw + lane / g.K;
         const int cn = q < g.n_rays ? L.cand_n[(size_t)q * g.K + g.j] : SEG_SKIP;
-        seg_first_item(L, L.scene, g, t, cn, stride, fault, c);
+        int2 out;
+        int ocn;
+        seg_first_item(L, L.scene, g, t, cn, stride, fault, c, out, ocn);
     }
 }
 
@@ -2249,11 +2273,47 @@ __global__ void __launch_bounds__(256, MINW) k_walk_first(RtLaunch L)
     }
 }
 
+// The shading of one resolved segment (k_shade, k_seg): the pixel is written when the ray ends, a
+// continuation is queued for the next level, an overflowed list (cn < 0) goes to k_cont.  `fh` =
+// first[ray] (k_first's {node, slot}).
+__device__ __forceinline__ void shade_ray(const RtLaunch &L, const RtFrameSetup &F, const RayQueues &Q, const RaySrc &src,
+                                          int cn, int2 fh, Counters &c)
+{
+    RayResult R;
+    if (F.fault) {
+        R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.segments = 1; R.status = ST_FAULT;
+        write_pixel(L, (size_t)src.pix, R);
+        return;
+    }
+    if (cn < 0) {
+        // the candidate list overflowed: the fused kernel traces this ray (from its segment start)
+        if (src.rec) {
+            const int k = wave_reserve(L.ctr);
+            L.ovf[k] = *src.rec;
+        } else {
+            R.hit_ent = -1; R.hit_node = -1; R.segments = 1;
+            queue_push(L.ovf, L.ctr, src.o, src.d, 1, 1, 1, 0, 0, F.start_sub, R, src.pix, 1, 0u);
+        }
+        return;
+    }
+    const ListHit pre = {fh.x, fh.y, fh.y >= 0 ? L.scene.prim[fh.y].rank : 0};
+    trace_ray<false, TR_LIST>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, cn, pre, src.rec, Q,
+                              src.pix, L);
+    if (R.status == ST_DEFER) return;
+    write_pixel(L, (size_t)src.pix, R);
+}
+
+__device__ __forceinline__ bool seg_shaded(const RtLaunch &L)
+{
+    return RT_SEG_FUSED && RT_SEG_SHADE && L.level >= 1 && seg_mode(L);
+}
+
 // Pass 3: shading of the resolved segment; pixels whose ray ends are written, continuations are
 // queued for the next level, overflowed lists go to the fused kernel (k_cont).
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
 {
+    if (seg_shaded(L)) return;                    // k_seg shaded this segmented level
     const int lane = threadIdx.x & 63;
     const int items = n_items(L);
     const RtFrameSetup F = *L.setup;
@@ -2278,30 +2338,11 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
             ray_src(L, t, lane, src);
         }
         if (!src.valid) continue;
-        RayResult R;
         if (F.fault) {
-            R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.segments = 1; R.status = ST_FAULT;
-            write_pixel(L, (size_t)src.pix, R);
+            shade_ray(L, F, Q, src, 0, make_int2(-1, -1), c);
             continue;
         }
-        const int cn = ray_cn[src.id];
-        if (cn < 0) {
-            // the candidate list overflowed: the fused kernel traces this ray (from its segment start)
-            if (src.rec) {
-                const int k = wave_reserve(L.ctr);
-                L.ovf[k] = *src.rec;
-            } else {
-                R.hit_ent = -1; R.hit_node = -1; R.segments = 1;
-                queue_push(L.ovf, L.ctr, src.o, src.d, 1, 1, 1, 0, 0, F.start_sub, R, src.pix, 1, 0u);
-            }
-            continue;
-        }
-        const int2 fh = reinterpret_cast<const int2 *>(L.first)[src.id];
-        const ListHit pre = {fh.x, fh.y, fh.y >= 0 ? L.scene.prim[fh.y].rank : 0};
-        trace_ray<false, TR_LIST>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, cn, pre, src.rec, Q,
-                                  src.pix, L);
-        if (R.status == ST_DEFER) continue;
-        write_pixel(L, (size_t)src.pix, R);
+        shade_ray(L, F, Q, src, ray_cn[src.id], reinterpret_cast<const int2 *>(L.first)[src.id], c);
         }
     }
 }
@@ -2460,7 +2501,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             // mode as seg_mode / refill_level do and launches the kernels that will return with
             // NO_OP_BLOCKS blocks: a persistent pass is correct at any grid, so a wrong prediction only
             // costs time, and a small part's frame no longer dispatches full grids that do nothing.
-            int mb_plain = mb, mb_seg = mb, mb_refill = mb, mb_first = mb, mb_first_seg = mb;
+            int mb_plain = mb, mb_seg = mb, mb_refill = mb, mb_first = mb, mb_first_seg = mb, mb_shade = mb;
             if (lv >= 1 && hint >= 0 && RT_NO_OP_BLOCKS > 0) {
                 const long long P = (long long)L.rows * (long long)L.cam.width;
                 const bool seg = L.seg > 1 && (L.seg_max <= 0 || hint <= L.seg_max) && (long long)hint * L.seg <= P;
@@ -2468,6 +2509,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
                 while (g < 64 && (long long)g * 4096 < (long long)hint) g *= 2;
                 const bool refill = !seg && Lv.refill > 0 && g >= 64;
                 if (seg) mb_plain = mb_refill = mb_first = RT_NO_OP_BLOCKS;
+                if (seg && RT_SEG_FUSED && RT_SEG_SHADE) mb_shade = RT_NO_OP_BLOCKS;   // k_seg shades it
                 else mb_seg = mb_first_seg = RT_NO_OP_BLOCKS;
                 if (refill) mb_plain = RT_NO_OP_BLOCKS;
                 else mb_refill = RT_NO_OP_BLOCKS;
@@ -2490,7 +2532,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             HIP_TRY(hipGetLastError());
             if (RT_FIRST_REFILL && lv >= 1 && Lv.refill > 0) launch_persistent(k_first_refill<6>, st, Lv, mb);
             if (lv >= 1 && L.seg > 1 && !RT_SEG_FUSED) launch_persistent(k_first_seg<4>, st, Lv, mb_first_seg);
-            launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv, mb);
+            launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv, mb_shade);
             HIP_TRY(hipGetLastError());
         }
         launch_persistent(k_cont<3>, st, L, level_blocks(L, L.ctr_hint ? L.ctr_hint[0] : -1));
