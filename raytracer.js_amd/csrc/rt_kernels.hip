@@ -2509,8 +2509,8 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
                 while (g < 64 && (long long)g * 4096 < (long long)hint) g *= 2;
                 const bool refill = !seg && Lv.refill > 0 && g >= 64;
                 if (seg) mb_plain = mb_refill = mb_first = RT_NO_OP_BLOCKS;
-                if (seg && RT_SEG_FUSED && RT_SEG_SHADE) mb_shade = RT_NO_OP_BLOCKS;   // k_seg shades it
                 else mb_seg = mb_first_seg = RT_NO_OP_BLOCKS;
+                if (seg && RT_SEG_FUSED && RT_SEG_SHADE) mb_shade = RT_NO_OP_BLOCKS;   // k_seg shades it
                 if (refill) mb_plain = RT_NO_OP_BLOCKS;
                 else mb_refill = RT_NO_OP_BLOCKS;
             }
