@@ -1860,7 +1860,7 @@ __device__ __forceinline__ void seg_first_item(const RtLaunch &L, const RtDevSce
 #define RT_SEG_FUSED 1
 #endif
 #ifndef RT_SEG_SHADE
-#define RT_SEG_SHADE 0                 // k_seg also shades its level (k_shade skips the level)
+#define RT_SEG_SHADE 1                 // k_seg also shades its level (k_shade skips the level)
 #endif
 __device__ __forceinline__ void shade_ray(const RtLaunch &L, const RtFrameSetup &F, const RayQueues &Q, const RaySrc &src,
                                           int cn, int2 fh, Counters &c);

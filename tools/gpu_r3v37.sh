@@ -1,5 +1,5 @@
 set -u
-OUT=gpurun_out/r3v36
+OUT=gpurun_out/r3v37
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1
 RT_LIB=$PWD/raytracer.js_amd/lib/librt_amd_segshade.so timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1 || exit $?
