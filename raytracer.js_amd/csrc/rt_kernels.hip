@@ -1860,14 +1860,21 @@ __device__ __forceinline__ void seg_first_item(const RtLaunch &L, const RtDevSce
 #define RT_SEG_FUSED 1
 #endif
 #ifndef RT_SEG_SHADE
-#define RT_SEG_SHADE 1                 // k_seg also shades its level (k_shade skips the level)
+#define RT_SEG_SHADE 1                 // k_seg also shades levels of up to RT_SEG_SHADE_MAX rays (k_shade skips them)
 #endif
+#ifndef RT_SEG_SHADE_MAX
+#define RT_SEG_SHADE_MAX 32768         // = the rays k_shade would take 8 per wave (cont_g); wider levels keep
+#endif                                 // k_shade's wider waves and k_seg's 4-wave occupancy
 __device__ __forceinline__ void shade_ray(const RtLaunch &L, const RtFrameSetup &F, const RayQueues &Q, const RaySrc &src,
                                           int cn, int2 fh, Counters &c);
-template <int MINW>
+__device__ __forceinline__ bool seg_shaded(const RtLaunch &L)
+{
+    return RT_SEG_FUSED && RT_SEG_SHADE && L.level >= 1 && seg_mode(L) && *lvl_ctr(L, L.level - 1) <= RT_SEG_SHADE_MAX;
+}
+template <int MINW, bool SHADE>
 __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
 {
-    if (!seg_mode(L)) return;
+    if (!seg_mode(L) || seg_shaded(L) != SHADE) return;     // the other instantiation takes this level
     stage_top(L.scene);
     const int lane = threadIdx.x & 63;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1886,7 +1893,7 @@ __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
         int2 out;
         int ocn;
         seg_first_item(L, S, g, t, cn, stride, fault, c, out, ocn);
-        if (RT_SEG_SHADE) {
+        if (SHADE) {
             // the ray's shading, by the lane of its segment 0 (k_shade's work for this ray)
             const int q = t * g.rpw + lane / g.K;
             if (q < g.n_rays && g.j == 0) {
@@ -2303,11 +2310,6 @@ __device__ __forceinline__ void shade_ray(const RtLaunch &L, const RtFrameSetup 
     write_pixel(L, (size_t)src.pix, R);
 }
 
-__device__ __forceinline__ bool seg_shaded(const RtLaunch &L)
-{
-    return RT_SEG_FUSED && RT_SEG_SHADE && L.level >= 1 && seg_mode(L);
-}
-
 // Pass 3: shading of the resolved segment; pixels whose ray ends are written, continuations are
 // queued for the next level, overflowed lists go to the fused kernel (k_cont).
 template <int MINW>
@@ -2502,6 +2504,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             // NO_OP_BLOCKS blocks: a persistent pass is correct at any grid, so a wrong prediction only
             // costs time, and a small part's frame no longer dispatches full grids that do nothing.
             int mb_plain = mb, mb_seg = mb, mb_refill = mb, mb_first = mb, mb_first_seg = mb, mb_shade = mb;
+            int mb_seg_shade = mb, mb_seg_wide = mb;
             if (lv >= 1 && hint >= 0 && RT_NO_OP_BLOCKS > 0) {
                 const long long P = (long long)L.rows * (long long)L.cam.width;
                 const bool seg = L.seg > 1 && (L.seg_max <= 0 || hint <= L.seg_max) && (long long)hint * L.seg <= P;
@@ -2510,7 +2513,9 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
                 const bool refill = !seg && Lv.refill > 0 && g >= 64;
                 if (seg) mb_plain = mb_refill = mb_first = RT_NO_OP_BLOCKS;
                 else mb_seg = mb_first_seg = RT_NO_OP_BLOCKS;
-                if (seg && RT_SEG_FUSED && RT_SEG_SHADE) mb_shade = RT_NO_OP_BLOCKS;   // k_seg shades it
+                const bool shaded = seg && RT_SEG_FUSED && RT_SEG_SHADE && hint <= RT_SEG_SHADE_MAX;
+                if (shaded) mb_shade = mb_seg_wide = RT_NO_OP_BLOCKS;   // k_seg<.., true> shades the level
+                else mb_seg_shade = RT_NO_OP_BLOCKS;
                 if (refill) mb_plain = RT_NO_OP_BLOCKS;
                 else mb_refill = RT_NO_OP_BLOCKS;
             }
@@ -2523,7 +2528,10 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
             if (lv >= 1 && L.seg > 1) {                 // one of the two runs (§5.10)
-                if (RT_SEG_FUSED) launch_persistent(k_seg<2>, st, Lw, mb_seg, lds);
+                if (RT_SEG_FUSED) {
+                    launch_persistent(k_seg<2, false>, st, Lw, std::min(mb_seg, mb_seg_wide), lds);
+                    if (RT_SEG_SHADE) launch_persistent(k_seg<2, true>, st, Lw, std::min(mb_seg, mb_seg_shade), lds);
+                }
                 else launch_persistent(k_walk_seg<2>, st, Lw, mb_seg, lds);
             }
             if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<RT_REFILL_OCC>, st, Lw, mb_refill, lds);
