@@ -2543,7 +2543,10 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv, mb_shade);
             HIP_TRY(hipGetLastError());
         }
-        launch_persistent(k_cont<3>, st, L, level_blocks(L, L.ctr_hint ? L.ctr_hint[0] : -1));
+        // k_cont: a recent frame with no ray left over predicts none now (NO_OP_BLOCKS still finish any)
+        const int32_t cont_hint = L.ctr_hint ? L.ctr_hint[0] : -1;
+        launch_persistent(k_cont<3>, st, L,
+                          cont_hint == 0 && RT_NO_OP_BLOCKS > 0 && L.lv_blocks <= 0 ? RT_NO_OP_BLOCKS : level_blocks(L, cont_hint));
         // this frame's counters come back for the next frames' grid hints (any recent frame will do)
         if (L.ctr_out) {
             HIP_TRY(hipMemcpyAsync(L.ctr_out, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
