@@ -33,6 +33,32 @@ constexpr int ST_DEFER = 100;                    // split path: continuation que
 #endif
 constexpr int STEP_CAP = 1 << 24;                // per-walk loop bound: every lane terminates
 
+// RT_TL builds (-DRT_TL=1, tools/tl_probe.py): a device-side timeline of every launch, for the
+// frames-in-flight analysis of small parts, where rocprofv3's kernel trace makes the
+// host the bottleneck.  Lane 0 of every wave takes the launch's record's start (minimum) and end
+// (maximum) of the 100 MHz wall clock; the host numbers launches and names them.
+#ifndef RT_TL
+#define RT_TL 0
+#endif
+#if RT_TL
+enum { RT_TL_MAX = 1 << 16 };
+__device__ unsigned long long g_tl[RT_TL_MAX][2];
+struct TlScope {
+    int id;
+    __device__ explicit TlScope(int i) : id(i)
+    {
+        if (id >= 0 && (threadIdx.x & 63) == 0) atomicMin(&g_tl[id][0], (unsigned long long)wall_clock64());
+    }
+    __device__ ~TlScope()
+    {
+        if (id >= 0 && (threadIdx.x & 63) == 0) atomicMax(&g_tl[id][1], (unsigned long long)wall_clock64());
+    }
+};
+#define TL_SCOPE(i) TlScope tl_scope_(i)
+#else
+#define TL_SCOPE(i) (void)0
+#endif
+
 // ---- node access --------------------------------------------------------------------------------
 struct NodeDims { double x, y, z, s; };
 
@@ -1141,8 +1167,9 @@ __device__ __forceinline__ void rotate_1(double &x, double &y, double c, double 
 __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
                                                      RtFrameSetup *setup, int part, int n_parts, int stripe,
                                                      int rows, int row0, double *__restrict__ dirs, int32_t *ctr,
-                                                     int32_t *fault)
+                                                     int32_t *fault, int tl)
 {
+    TL_SCOPE(tl);
     const int lane = threadIdx.x & 63;
     if (blockIdx.x == 0) {
         // the frame's work counters (and, when asked, its fault flag) start at zero: the frame's later
@@ -1168,12 +1195,15 @@ __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_des
             cur = reinterpret_cast<const int2 *>(S.node_up)[cur].x;
         }
         if (lane == 0) {
-            RtFrameSetup f;
-            f.fault = r < 0;
-            f.start_tree = r == 1 ? t : -1;
-            f.start_oct = oc;
-            f.start_sub = se >= 0 ? S.ent_sub[se] : cfg.default_substance;
-            *setup = f;
+            setup->fault = r < 0;
+            setup->start_tree = r == 1 ? t : -1;
+            setup->start_oct = oc;
+            setup->start_sub = se >= 0 ? S.ent_sub[se] : cfg.default_substance;
+            int n = 0;
+            for (int a = r == 1 ? t : -1; a >= 0 && n <= RT_CHAIN; a = reinterpret_cast<const int2 *>(S.node_up)[a].x)
+                if (n < RT_CHAIN) setup->chain[n++] = a;
+                else n = RT_CHAIN + 1;
+            setup->n_chain = n > RT_CHAIN ? -1 : n;
         }
         return;
     }
@@ -1653,6 +1683,7 @@ __device__ __forceinline__ void pixel_src(const RtLaunch &L, int id, RaySrc &r)
 template <bool STATS, int MINW>
 __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
     const int n_tiles = n_items(L);
     const RtFrameSetup F = *L.setup;
@@ -1874,6 +1905,7 @@ __device__ __forceinline__ bool seg_shaded(const RtLaunch &L)
 template <int MINW, bool SHADE>
 __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     if (!seg_mode(L) || seg_shaded(L) != SHADE) return;     // the other instantiation takes this level
     stage_top(L.scene);
     const int lane = threadIdx.x & 63;
@@ -1913,6 +1945,7 @@ __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     if (!seg_mode(L)) return;
     stage_top(L.scene);
     const int lane = threadIdx.x & 63;
@@ -1931,6 +1964,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     if (!seg_mode(L)) return;
     const int lane = threadIdx.x & 63;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1970,6 +2004,7 @@ __device__ __forceinline__ bool refill_level(const RtLaunch &L)
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     if (!refill_level(L)) return;
     stage_top(L.scene);
     constexpr int IDLE = 9;
@@ -2060,6 +2095,7 @@ __device__ __forceinline__ int walk_item(const RtLaunch &L, const RtDevScene &S,
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
     const int items = n_items(L);
     const RtFrameSetup F = *L.setup;
@@ -2142,6 +2178,7 @@ __device__ __forceinline__ bool early_shade(const RtLaunch &L, const RaySrc &src
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_first_refill(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     if (!RT_FIRST_REFILL || !refill_level(L)) return;
     const int lane = threadIdx.x & 63;
     const RtDevScene &S = L.scene;
@@ -2231,6 +2268,7 @@ __device__ __forceinline__ void first_finish(const RtLaunch &L, const RaySrc &sr
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
     const int items = n_items(L);
     const RtDevScene &S = L.scene;
@@ -2261,6 +2299,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_first(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
     const int items = n_items(L);
     const RtFrameSetup F = *L.setup;
@@ -2277,6 +2316,134 @@ __global__ void __launch_bounds__(256, MINW) k_walk_first(RtLaunch L)
         if (!src.valid) continue;
         const int cn = walk_item(L, S, F, src, stride, c);
         first_item<false>(L, S, src, cn, (uint32_t)stride, F.fault != 0, c);
+    }
+}
+
+// Level 0 of a small part with segmented primary rays (L.l0_seg = K > 1).  A part
+// of an 8-GPU frame has about one 8x8 tile per resident wave, so k_walk_first's time is its slowest
+// tile.  Here each primary ray is cut into K segments along its root-cube crossing exactly as the
+// bounce levels' rays are (§5.10: segment 0 is the reference walk from the camera's seat, segment
+// j >= 1 is seated in the slot holding the point at j/K of the crossing, and each stops on reaching
+// the next valid segment's seat), and a wave takes 64 / K rays of an 8 x (8 / K) pixel tile with K
+// adjacent lanes per ray: K times more work items, each about 1/K of a tile's walk.  The wave then
+// scans its segments' lists (seg_first_item's rule: a segment is scanned only if every earlier one
+// reached its successor), and the lane of each ray's segment 0 finishes the ray as first_item does
+// (early_shade, or the level-0 shading queue), with the combined end status in cand_n[pixel] for
+// k_shade.  Lists: ray pixel * K + segment, stride K * pixels (prepare sizes the buffer).
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_walk_first_seg(RtLaunch L)
+{
+    TL_SCOPE(L.tl);
+    const int lane = threadIdx.x & 63;
+    const RtFrameSetup F = *L.setup;
+    const RtDevScene &S = L.scene;
+    const int K = L.l0_seg, th = 8 / K;                      // K in {2, 4, 8}: tiles of 8 x th pixels
+    const int W = L.cam.width;
+    const int tiles_x = (W + 7) >> 3;
+    const int items = tiles_x * ((L.rows + th - 1) / th);
+    const size_t P = (size_t)L.rows * (size_t)W;
+    const uint32_t stride = (uint32_t)(P * (size_t)K);
+    const int j = lane & (K - 1), base = lane & ~(K - 1), r = lane / K;
+    const double frac = (double)j / (double)K;
+    const bool fault = F.fault != 0;
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    stage_top(S);
+    for (;;) {
+        int t_end;
+        const int t = claim_xcd(pass_heads(L, 0, 1), items, lane, 1, t_end, L.xcd_mask & 1);
+        if (t >= items) break;
+        const int ty = t / tiles_x, tx = t - ty * tiles_x;
+        const int x = tx * 8 + (r & 7), lr = ty * th + (r >> 3);
+        const bool valid = x < W && lr < L.rows;
+        RaySrc src;
+        src.valid = valid;
+        src.rec = nullptr;
+        src.id = valid ? (size_t)lr * (size_t)W + (size_t)x : 0;
+        src.pix = (int)src.id;
+        for (int i = 0; i < 3; i++) {
+            src.o[i] = L.cam.pos[i];
+            src.d[i] = valid ? L.dirs[(size_t)i * P + (size_t)x * (size_t)L.rows + (size_t)lr] : 1.0;   // x-major
+        }
+        const uint32_t id = (uint32_t)(src.id * (size_t)K + (size_t)j);
+        // this lane's segment: its seat, or none (SEG_SKIP)
+        Walker w;
+        int end = SEG_SKIP, seat = -1;
+        if (valid) {
+            if (j == 0) {
+                end = !fault && walker_set(S, w, src.o, src.d, F.start_tree >= 0, F.start_tree, F.start_oct, c) >= 0
+                          ? SEG_FIN : SEG_THROW;
+            } else if (!fault && F.start_tree >= 0) {
+                const NodeDims rt = node_dims(S, 0);
+                BoxIsect bi;
+                if (box_isect(rt.x + 0.5 * rt.s, rt.y + 0.5 * rt.s, rt.z + 0.5 * rt.s, rt.s, src.o, src.d, bi)) {
+                    const double t0 = bi.u1 > 0 ? bi.u1 : 0.0, t1 = bi.u2;
+                    if (t1 > t0 && t1 < 1e300) {
+                        const double tt = t0 + (t1 - t0) * frac;
+                        const double p[3] = {src.o[0] + src.d[0] * tt, src.o[1] + src.d[1] * tt, src.o[2] + src.d[2] * tt};
+                        int tree = -1, oct = 0;
+                        if (node_at_pos(S, p, tree, oct, c.loc) == 1 &&
+                            walker_set(S, w, src.o, src.d, true, tree, oct, c) >= 0) {
+                            seat = tree * 8 + oct;
+                            end = SEG_FIN;
+                        }
+                    }
+                }
+            }
+        }
+        int stop = -1;                                   // the seat of the next segment that has one
+        for (int k = 1; k < K; k++) {
+            const int s = __shfl(seat, base | (j + k < K ? j + k : K - 1), 64);
+            if (stop < 0 && j + k < K && s >= 0) stop = s;
+        }
+        int n = 0;
+        if (end == SEG_FIN) {
+            const RayBox rb = make_raybox(w.o, w.d);
+            // A segment j >= 1 returns the ancestors of its seat when it climbs out of them (a step_back
+            // at depth 0: F_STEPPED is set when the next head returns the slot's node).  An ancestor
+            // that does not hold the camera's seat was entered, and returned, by the reference walk
+            // before it reached this seat: its entities were tested and missed, so the list drops it.
+            // The camera seat's own ancestors are returned on the way out by the reference too: kept.
+            const int n_chain = F.n_chain;
+            auto emit = [&](int node) {
+                if (j > 0 && (w.flags & F_STEPPED) && n_chain >= 0) {
+                    bool cam = false;
+                    for (int a = 0; a < n_chain; a++) cam = cam || L.setup->chain[a] == node;
+                    if (!cam) return;
+                }
+                if (!node_candidate(S, node, L.cull != 0, rb)) return;
+                if (n < L.cand_cap) cand_store(L, n, stride, id, node);
+                n++;
+            };
+            const int rr = walker_run<true>(S, w, emit, stop);
+            if (rr < 0) end = rr == -2 ? SEG_CAP : SEG_THROW;
+            else if (rr == 2) end = SEG_REACHED;
+        }
+        const int cn = valid ? (n > L.cand_cap ? -1 : n * 8 + end) : SEG_SKIP;
+        // the scan of this lane's list if every earlier segment of the ray reached its successor
+        bool open = true;
+        for (int k = 0; k < K - 1; k++) {
+            const int s = __shfl(cn, base | k, 64);
+            if (k < j && !(s >= 0 && ((s & 7) == SEG_REACHED || (s & 7) == SEG_SKIP))) open = false;
+        }
+        int2 res = make_int2(-1, -1);
+        if (valid && open && cn >= 8 && !fault)
+            res = scan_first<false>(L, S, src.o, src.d, make_raybox(src.o, src.d), stride, id, cn >> 3, c);
+        // in segment order: an overflow sends the ray to k_cont; a hit wins; an end ends the ray
+        bool done = false;
+        int2 out = make_int2(-1, -1);
+        int ocn = 0;
+        for (int k = 0; k < K; k++) {
+            const int s = __shfl(cn, base | k, 64);
+            const int rx = __shfl(res.x, base | k, 64), ry = __shfl(res.y, base | k, 64);
+            if (done) continue;
+            if (s < 0) { done = true; ocn = -1; }
+            else if (ry >= 0) { done = true; out = make_int2(rx, ry); ocn = 4; }
+            else if ((s & 7) != SEG_REACHED && (s & 7) != SEG_SKIP) { done = true; ocn = s & 3; }
+        }
+        if (valid && j == 0) {
+            L.cand_n[src.id] = ocn;                      // k_shade's level-0 status (-1 overflow, end & 3)
+            first_finish(L, src, ocn, out, fault);
+        }
     }
 }
 
@@ -2315,6 +2482,7 @@ __device__ __forceinline__ void shade_ray(const RtLaunch &L, const RtFrameSetup 
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     if (seg_shaded(L)) return;                    // k_seg shaded this segmented level
     const int lane = threadIdx.x & 63;
     const int items = n_items(L);
@@ -2354,6 +2522,7 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
 {
+    TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
     const int n = L.ctr[0];
     const RtFrameSetup F = *L.setup;
@@ -2409,9 +2578,26 @@ __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, doub
 // makes an over-estimate harmless (late blocks find the queue empty).  The CU count and each
 // kernel's blocks per CU are queried once (all devices of a context are MI355X): one host thread
 // issues the launches of up to 8 GPUs, so a launch is only the launch.
-static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const RtLaunch &L, int max_blocks = 0,
+// RT_TL builds: launch id -> (kernel expression, stream); ids wrap at RT_TL_MAX (the reader resets)
+#if RT_TL
+static std::mutex g_tl_mu;
+static std::vector<std::pair<const void *, void *>> g_tl_host;
+static int tl_next(const void *name, hipStream_t st)
+{
+    std::lock_guard<std::mutex> g(g_tl_mu);
+    if (g_tl_host.size() >= (size_t)RT_TL_MAX) return -1;
+    g_tl_host.emplace_back(name, (void *)st);
+    return (int)g_tl_host.size() - 1;
+}
+#else
+static int tl_next(const void *, hipStream_t) { return -1; }
+#endif
+
+static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const RtLaunch &L0, int max_blocks = 0,
                               size_t lds = 0)
 {
+    RtLaunch L = L0;
+    L.tl = tl_next(reinterpret_cast<const void *>(kernel), st);
     static std::atomic<int> cus{0};
     static std::mutex mu;
     static std::vector<std::pair<std::pair<const void *, size_t>, int>> per_kernel;
@@ -2466,7 +2652,8 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     const bool trace = L.rows > 0 && !L.skip_trace;
     hipLaunchKernelGGL(k_frame_start, dim3(1 + (rg_lanes + 255) / 256), dim3(256), 0, st, L.scene, L.cam, L.cfg,
                        L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.row0, L.dirs, trace ? L.ctr : nullptr,
-                       L.zero_fault ? L.fault : nullptr);
+                       L.zero_fault ? L.fault : nullptr,
+                       tl_next(reinterpret_cast<const void *>(k_frame_start), st));
     HIP_TRY(hipGetLastError());
     if (!trace) {                                // an empty part (more devices than stripes): no trace
         if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
@@ -2523,7 +2710,8 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             RtLaunch Lw = Lv;                         // the walk kernels read the upper levels from LDS
             Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
             const size_t lds = sizeof(RtNode) * (size_t)Lw.scene.n_lds;
-            if (L.walk_first && lv == 0) launch_persistent(k_walk_first<4>, st, Lw, mb, lds);
+            if (L.l0_seg > 1 && lv == 0) launch_persistent(k_walk_first_seg<4>, st, Lw, mb, lds);
+            else if (L.walk_first && lv == 0) launch_persistent(k_walk_first<4>, st, Lw, mb, lds);
             else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb_plain, lds);
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
@@ -2570,6 +2758,57 @@ int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[
                            max_out, d_tree, d_oct, d_n);
     HIP_TRY(hipGetLastError());
     return RT_OK;
+}
+
+// RT_TL builds: the launches recorded since the last reset — start / end (100 MHz wall clock) of each,
+// its kernel expression (up to 63 characters) and stream — then (reset) a new timeline.  Returns the
+// count, or RT_E_UNSUPPORTED in production builds.
+extern "C" int rt_debug_timeline(int32_t max, unsigned long long *start_end, char *names, unsigned long long *streams,
+                                 int32_t reset)
+{
+#if RT_TL
+    std::lock_guard<std::mutex> g(g_tl_mu);
+    const int n = (int)std::min<size_t>(g_tl_host.size(), (size_t)std::max(0, max));
+    if (n > 0) {
+        if (hipDeviceSynchronize() != hipSuccess) return RT_E_HIP;
+        std::vector<unsigned long long> v(2 * (size_t)n);
+        if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_tl), sizeof(unsigned long long) * 2 * n) != hipSuccess)
+            return RT_E_HIP;
+        static const std::pair<const void *, const char *> known[] = {
+            {(const void *)k_frame_start, "k_frame_start"}, {(const void *)k_trace<true, 2>, "k_trace"},
+            {(const void *)k_trace<false, 2>, "k_trace"}, {(const void *)k_trace<false, 3>, "k_trace"},
+            {(const void *)k_trace<false, 4>, "k_trace"}, {(const void *)k_walk_first<4>, "k_walk_first"},
+            {(const void *)k_walk_first_seg<4>, "k_walk_first_seg"}, {(const void *)k_walk<3>, "k_walk"},
+            {(const void *)k_walk<4>, "k_walk"}, {(const void *)k_walk<5>, "k_walk"},
+            {(const void *)k_seg<2, false>, "k_seg_wide"}, {(const void *)k_seg<2, true>, "k_seg"},
+            {(const void *)k_walk_seg<2>, "k_walk_seg"}, {(const void *)k_walk_refill<RT_REFILL_OCC>, "k_walk_refill"},
+            {(const void *)k_first<4>, "k_first"}, {(const void *)k_first<6>, "k_first"}, {(const void *)k_first<8>, "k_first"},
+            {(const void *)k_first_refill<6>, "k_first_refill"}, {(const void *)k_first_seg<4>, "k_first_seg"},
+            {(const void *)k_shade<3>, "k_shade"}, {(const void *)k_shade<4>, "k_shade"}, {(const void *)k_shade<5>, "k_shade"},
+            {(const void *)k_cont<3>, "k_cont"}};
+        for (int i = 0; i < n; i++) {
+            start_end[2 * i] = v[2 * i];
+            start_end[2 * i + 1] = v[2 * i + 1];
+            const char *nm = "?";
+            for (const auto &k : known)
+                if (k.first == g_tl_host[i].first) nm = k.second;
+            snprintf(names + 64 * (size_t)i, 64, "%s", nm);
+            streams[i] = (unsigned long long)(uintptr_t)g_tl_host[i].second;
+        }
+    }
+    if (reset) {
+        if (hipDeviceSynchronize() != hipSuccess) return RT_E_HIP;
+        std::vector<unsigned long long> init(2 * (size_t)RT_TL_MAX);
+        for (size_t i = 0; i < init.size(); i += 2) { init[i] = ~0ull; init[i + 1] = 0; }
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tl), init.data(), sizeof(unsigned long long) * init.size()) != hipSuccess)
+            return RT_E_HIP;
+        g_tl_host.clear();
+    }
+    return n;
+#else
+    (void)max; (void)start_end; (void)names; (void)streams; (void)reset;
+    return RT_E_UNSUPPORTED;
+#endif
 }
 
 // RT_WALK_PROF builds: read (and optionally clear) the walk-loop profile (tools/walk_profile.py).

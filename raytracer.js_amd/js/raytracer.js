@@ -263,7 +263,12 @@ function shade_tables(shades, shade_index, image_of) {
 // per-object state is added to entities); the wrapper notes the object in every live Raytracer's
 // journal before the original runs.  invalidate_scene() then sends only the noted nodes and the sets
 // holding noted entities (rt_apply_edit), not the whole scene.
+// A Raytracer that is dropped without close() cannot be seen going away on Node 12 (no WeakRef), so a
+// journal bounds itself: past `cap` noted objects it forgets them and marks itself `over`, which
+// makes its Raytracer's next sync a full re-read, and every later mutator call skips it.  Where
+// FinalizationRegistry exists, a collected Raytracer's journal also leaves JOURNALS.
 const JOURNALS = new Set();
+const JOURNAL_GC = typeof FinalizationRegistry === 'function' ? new FinalizationRegistry((j) => JOURNALS.delete(j)) : null;
 const WRAPPED = Symbol('rt_journal_wrapped');
 const ENTITY_MUTATORS = ['_set_pos', 'set_material', 'set_texture', 'set_substance', 'set_diameter', 'set_size'];
 
@@ -275,7 +280,13 @@ function wrap_method(obj, name, note) {
 	if (!p || p === Object.prototype || typeof p[name] !== 'function' || p[name][WRAPPED]) return;
 	const orig = p[name];
 	const w = function () {
-		if (JOURNALS.size) for (const j of JOURNALS) note(j, this, arguments);
+		if (JOURNALS.size) for (const j of JOURNALS) if (!j.over) {
+			note(j, this, arguments);
+			if (j.nodes.size + j.ents.size + j.struct.size > j.cap) {
+				j.over = true;
+				j.nodes.clear(); j.ents.clear(); j.struct.clear();
+			}
+		}
 		return orig.apply(this, arguments);
 	};
 	w[WRAPPED] = true;
@@ -291,6 +302,15 @@ function journal_classes(node, entity) {
 			if (args[0]) j.nodes.add(args[0]);
 		});
 		for (const m of ENTITY_MUTATORS) wrap_method(entity, m, (j, e) => j.ents.add(e));
+	}
+}
+
+// The mutators of every entity class in `ents` (once per prototype; wrap_method skips wrapped ones)
+function wrap_entity_classes(ents) {
+	const seen = new Set();
+	for (const e of ents) {
+		const p = Object.getPrototypeOf(e);
+		if (!seen.has(p)) { seen.add(p); journal_classes(null, e); }
 	}
 }
 
@@ -460,6 +480,7 @@ function build_edit(scene, st, j, default_substance, sky_texture) {
 		for (let i = 0; i < scene.entities.length && !scatter; i++)
 			if (st.ent_shade[i] >= 0 && rough[st.ent_shade[i]] && entity_node(scene.entities[i]) != undefined) scatter = 1;
 	return Object.assign({
+		new_ents,                                        // (not read by the addon) their classes get journaled
 		n_slots: st.n_slots, n_entities: scene.entities.length,
 		rec_slot, rec_cube, rec_child, rec_up, set_slot, set_begin, set_count, set_ent, set_type, set_shade, set_geom,
 		sub_ent, sub_val, dfs_new_slot, dfs_new_val, dfs_shift, scatter,
@@ -564,17 +585,24 @@ class Raytracer {
 		}
 		this._st = st;
 		if (!this._journal) {
-			this._journal = { nodes: new Set(), ents: new Set(), struct: new Set() };
+			this._journal = { nodes: new Set(), ents: new Set(), struct: new Set(), over: false, cap: 0 };
 			JOURNALS.add(this._journal);
+			if (JOURNAL_GC) JOURNAL_GC.register(this, this._journal);
 		}
 		const j = this._journal;
 		j.nodes.clear(); j.ents.clear(); j.struct.clear();
-		const seen = new Set();
+		j.over = false;
+		j.cap = Math.max(1 << 16, n_slots + sc.entities.length);
 		journal_classes(this.otree, null);
-		for (const e of sc.entities) {
-			const p = Object.getPrototypeOf(e);
-			if (!seen.has(p)) { seen.add(p); journal_classes(null, e); }
-		}
+		wrap_entity_classes(sc.entities);
+	}
+
+	// After rt_apply_edit took `edit`: a fresh journal, and the mutators of entity classes the last full
+	// read did not see (a sphere added to a box-only scene: SphereEntity._set_pos, set_diameter) wrapped
+	_edit_applied(edit) {
+		wrap_entity_classes(edit.new_ents);
+		const j = this._journal;
+		j.nodes.clear(); j.ents.clear(); j.struct.clear();
 	}
 
 	_sync_scene() {
@@ -593,18 +621,17 @@ class Raytracer {
 			this._begin_journal(sl.slots, sl.n_slots);
 		} else if (this._dirty) {
 			let u = null;
-			if (!this._full && this._st) {
+			if (!this._full && this._st && !this._journal.over) {
 				const t0 = process.hrtime();
 				const edit = build_edit(this._scene, this._st, this._journal, this.config.default_substance, sky);
 				const t1 = process.hrtime(t0);
 				if (edit) u = a.applyEdit(this._ctx, edit);     // null: the store asks for a full upload
 				if (u) {
+					this._edit_applied(edit);
 					const dt = process.hrtime(t0);
 					u.build_ms = t1[0] * 1e3 + t1[1] / 1e6;        // journal -> rt_edit_desc (JS)
 					u.js_ms = dt[0] * 1e3 + dt[1] / 1e6;          // ... -> applied (JS + addon + librt)
 					u.via = 'edit';
-					const j = this._journal;
-					j.nodes.clear(); j.ents.clear(); j.struct.clear();
 				}
 			}
 			if (!u) {

@@ -6,7 +6,10 @@
  * ids with the shift) and the result must equal a fresh serialize_scene of the edited tree, node by
  * node in DFS order: cube, parent, children, EntitySet (entity ids, types, geometry bits, shades),
  * substances.  ops: [{op: 'move', entity, pos, depth} | {op: 'add_sphere', pos, d, depth, like} |
- * {op: 'shade', entity, like} | {op: 'substance', entity, like}].  Prints 'edit ok' and a summary.
+ * {op: 'shade', entity, like} | {op: 'substance', entity, like} | {op: 'setpos', entity, pos} |
+ * {op: 'sync'}]: a 'sync' applies the
+ * edit so far as a frame would (the model takes it, the Raytracer's _edit_applied starts a new
+ * journal), so later ops form a second edit.  Prints 'edit ok' and a summary.
  */
 'use strict';
 const fs = require('fs');
@@ -38,7 +41,7 @@ const E = { type: Array.from(old.ent_type), geom: [], shade: Array.from(old.ent_
 for (let i = 0; i < old.ent_type.length; i++) E.geom[i] = Array.from(old.ent_geom.subarray(9 * i, 9 * i + 9));
 
 // the edits, through the mutators
-for (const o of ops) {
+function do_op(o) {
 	if (o.op === 'move') {
 		const e = world.entities[o.entity];
 		e._set_pos({ v: o.pos });
@@ -47,6 +50,9 @@ for (const o of ops) {
 		const like = world.entities[o.like];
 		const e = new rs.SphereEntity(like.get_material(), like.get_texture(), like.get_substance(), o.pos, o.d);
 		rs.add_entity_to_octree(world.root, e, { max_in_depth: o.depth, max_out_depth: 0 });
+		world.entities.push(e);                             // later ops name it by this index
+	} else if (o.op === 'setpos') {                         // _set_pos alone: the entity stays in its node
+		world.entities[o.entity]._set_pos({ v: o.pos });
 	} else if (o.op === 'shade') {
 		const e = world.entities[o.entity], like = world.entities[o.like];
 		e.set_material(like.get_material());
@@ -55,6 +61,7 @@ for (const o of ops) {
 		world.entities[o.entity].set_substance(world.entities[o.like].get_substance());
 	} else throw Error('op ' + o.op);
 }
+function sync() {
 const edit = rt._internal.build_edit(tr._scene, tr._st, tr._journal, undefined, sky);
 assert(edit, 'build_edit refused an expressible edit');
 
@@ -84,6 +91,16 @@ for (let s = 0; s < old_slots; s++) {
 }
 for (let i = 0; i < edit.dfs_new_slot.length; i++) M.dfs[edit.dfs_new_slot[i]] = edit.dfs_new_val[i];
 assert.strictEqual(M.cube.length, edit.n_slots);
+tr._edit_applied(edit);
+return edit;
+}
+
+let edit = null;
+for (const o of ops) {
+	if (o.op === 'sync') edit = sync();
+	else do_op(o);
+}
+edit = sync();
 
 // a fresh linearisation of the edited tree (stable entity ids), compared node by node
 const neu = rt.serialize_scene(world.root, undefined, old, sky);
@@ -111,5 +128,5 @@ for (let k = 0; k < N1; k++) {
 		assert.strictEqual(E.sub[id], neu.ent_substance[id], 'substance ' + id);
 	}
 }
-console.log('edit ok: ' + JSON.stringify({ slots: edit.n_slots, new_nodes: edit.n_slots - old_slots, rec: edit.rec_slot.length,
+console.log('edit ok: ' + JSON.stringify({ slots: edit.n_slots, new_nodes: edit.n_slots - N0, rec: edit.rec_slot.length,
 	sets: edit.set_slot.length, members: edit.set_ent.length, subs: edit.sub_ent.length }));

@@ -67,6 +67,10 @@ EDIT_OPS = {
                         {"op": "shade", "entity": 3, "like": 1}, {"op": "substance", "entity": 7, "like": 1},
                         {"op": "move", "entity": 5, "pos": [0.5, 0.5, 0.5], "depth": 5}]),
     "config2_moves": ("config2", [{"op": "shade", "entity": 10, "like": 20}]),
+    # a sphere joins a box-only scene through the journal, then moves by its own _set_pos (which
+    # overrides the boxes' one): the second edit must see it
+    "new_class": ("boxes", [{"op": "add_sphere", "pos": [0.41, 0.37, 0.52], "d": 0.03, "depth": 6, "like": 0},
+                            {"op": "sync"}, {"op": "setpos", "entity": 11, "pos": [0.43, 0.36, 0.52]}]),
 }
 
 
@@ -76,11 +80,22 @@ def test_edit_journal_equals_fresh_linearisation(tmp_path, name):
     rt_apply_edit applies it (records, sets, substances, DFS ids and shift), equals a fresh
     serialize_scene of the edited tree (tests/js/check_edit.js)."""
     scene, ops = EDIT_OPS[name]
-    spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4), "config2": scenes.config2}[scene]()
+    spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4), "config2": scenes.config2,
+            "boxes": lambda: scenes.small_random(4, n_tri=0, n_sph=0, n_box=10)}[scene]()
     path = _dump(tmp_path, spec, scenes.make_camera(8, 8), scenes.make_config(2))
     (tmp_path / "ops.json").write_text(json.dumps(ops))
     out = _node([os.path.join(ROOT, "tests", "js", "check_edit.js"), path, str(tmp_path / "ops.json")])
     assert "edit ok" in out, out
+
+
+def test_journal_bounds_itself(tmp_path):
+    """CPU: a journal past its cap (a Raytracer dropped without close()) forgets its notes, marks
+    itself over (the next sync re-reads the scene) and is skipped by later mutator calls; a live
+    journal keeps noting (tests/js/check_journal_cap.js)."""
+    spec = scenes.small_random(4)
+    path = _dump(tmp_path, spec, scenes.make_camera(8, 8), scenes.make_config(2))
+    out = _node([os.path.join(ROOT, "tests", "js", "check_journal_cap.js"), path])
+    assert "journal cap ok" in out, out
 
 
 def test_addon_loads_and_fails_loudly_without_gpu():

@@ -30,8 +30,10 @@ def main():
     ap.add_argument("--parts", type=int, nargs="*", default=[1, 8])
     ap.add_argument("--inflight", type=int, nargs="*", default=[1, 2, 3])
     ap.add_argument("--frames", type=int, default=30)
+    ap.add_argument("--refmax", type=int, default=0, help="override the workload's refmax (0: keep)")
     a = ap.parse_args()
     factory, W, H, refmax = scenes.WORKLOADS[a.config]
+    refmax = a.refmax or refmax
     scene = rtamd.build_scene(factory())
     cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
     dev = torch.device("cuda", 0)
