@@ -463,8 +463,14 @@ def kernel_rooflines(dur, pmc, counters):
                      branch_insts=int(c.get("SQ_INSTS_BRANCH", 0)), valu_issue_cycles=int(cyc),
                      valu_issue_frac_peak_clock=round(cyc / (SIMDS * CLOCK_GHZ * 1e9 * s), 4))
             if c.get("GRBM_GUI_ACTIVE"):
+                # GRBM_GUI_ACTIVE counts GPU-busy cycles over the whole dispatch window, which for a
+                # short kernel includes other work: a "clock" above the 2.4 GHz peak is not a clock.
+                # The issue fraction is taken at min(measured, peak), and such values are flagged.
                 clk = c["GRBM_GUI_ACTIVE"] / 8 / s
-                e.update(clock_ghz=round(clk / 1e9, 3), valu_issue_frac=round(cyc / (SIMDS * clk * s), 4))
+                ok = clk <= CLOCK_GHZ * 1e9 * 1.02
+                use = min(clk, CLOCK_GHZ * 1e9)
+                e.update(clock_ghz=round(use / 1e9, 3), clock_ghz_counter=round(clk / 1e9, 3), clock_valid=ok,
+                         valu_issue_frac=round(cyc / (SIMDS * use * s), 4))
         if c.get("SQ_ACTIVE_INST_VALU"):
             lanes = c["SQ_THREAD_CYCLES_VALU"] / c["SQ_ACTIVE_INST_VALU"]
             e.update(active_lanes=round(lanes, 2), lane_util=round(lanes / 64, 4))
@@ -475,12 +481,34 @@ def kernel_rooflines(dur, pmc, counters):
             # the pass's algorithmic bytes are shared by its kernels in proportion to their time
             share = ms / sum(v for kk, v in dur.items() if pass_of.get(kk) == p)
             ab = algorithmic_bytes(counters, pass_bytes[p]) * share
-            e.update(alg_bytes_cache_served=int(ab), alg_GBps=round(ab / s / 1e9, 1))
+            # one pool of bytes per pass split by time share: an accounting identity across a pass's
+            # kernels (equal rates by construction), not a per-kernel measurement
+            e.update(alg_bytes_cache_served_pooled=int(ab), alg_GBps_pooled=round(ab / s / 1e9, 1),
+                     alg_frac_of_hbm_peak_pooled=round(ab / s / 1e9 / HBM_PEAK_GBS, 4))
         roofs = {r: e[f] for r, f in (("valu-issue", "valu_issue_frac"), ("hbm", "hbm_frac")) if f in e}
         if roofs:
             e["binding_roof"] = max(roofs, key=roofs.get)
         out[k] = e
     return out
+
+
+def hbm_8d(tot, s_per_frame, hbm_counted):
+    """SURVEY §8(d)'s HBM roofline frame, with why it does not apply: the reference-equivalent bytes
+    (what the reference's Set-order loop would read) and the kernels' own algorithmic bytes per frame,
+    each over the frame time, against 8 TB/s, beside the HBM bytes the counters saw.  The scene (26 MB
+    at config 3) is L2/MALL resident and the cull hierarchies replace ~700x more exact tests than they
+    run, so the first two exceed HBM peak by construction; VALU issue is the roof that binds."""
+    ref_b, alg_b = algorithmic_bytes(tot, BYTES_REF), algorithmic_bytes(tot, BYTES_KERNEL)
+    return dict(applicable=False,
+                reference_equivalent_bytes_per_frame=int(ref_b),
+                reference_equivalent_TBps=round(ref_b / s_per_frame / 1e12, 2),
+                reference_equivalent_frac_of_peak=round(ref_b / s_per_frame / 1e9 / HBM_PEAK_GBS, 2),
+                kernel_alg_bytes_per_frame=int(alg_b),
+                kernel_alg_TBps=round(alg_b / s_per_frame / 1e12, 2),
+                kernel_alg_frac_of_peak=round(alg_b / s_per_frame / 1e9 / HBM_PEAK_GBS, 2),
+                hbm_bytes_counted_per_frame=int(hbm_counted),
+                hbm_counted_frac_of_peak=round(hbm_counted / s_per_frame / 1e9 / HBM_PEAK_GBS, 4),
+                note="not the binding roof: cache-resident scene and culled entity tests; see roofline.kernels")
 
 
 def exposure_bench(ctx, frame, stream, reps=20):
@@ -525,27 +553,30 @@ def _host_frame_ms(ctx, cam, cfg, warm, reps):
 
 def host_frame_time(ctx, cam, cfg, segments, scene=None, device=0, warm=3, reps=10):
     """SURVEY §8(d) ms/frame: rt_trace_frame with a host Float32Array (camera in, kernels, D2H into
-    the ebuffer) — what the JS drop-in's trace_frame() costs.  Median of `reps` after `warm`.  The
-    context runs the frame as row bands on their own streams (RT_BANDS, default 2; DESIGN.md §5.14);
-    with `scene`, a second context with RT_BANDS=1 (one launch sequence, then one D2H) is timed
-    beside it and must produce the identical frame."""
+    the ebuffer) — what the JS drop-in's trace_frame() costs.  Median of `reps` after `warm`.  On one
+    GPU the frame streams to the host after level 0 (RT_HOST_STREAM); over several
+    GPUs each copies its own stripes (§7).  With `scene`, a second context with streaming off and one
+    band (one launch sequence, then one D2H) is timed beside it and must produce the identical frame."""
     ts, rgb = _host_frame_ms(ctx, cam, cfg, warm, reps)
     med = float(np.median(ts))
+    P = cam.width * cam.height
+    streamed = os.environ.get("RT_HOST_STREAM", "1") != "0" and P >= int(os.environ.get("RT_STREAM_MIN", str(1 << 20)))
     out = dict(entry="rt_trace_frame (host RGB buffer, D2H included)", warmup=warm, frames=reps,
-               bands=int(os.environ.get("RT_BANDS", "2")) if cam.width * cam.height >= int(
-                   os.environ.get("RT_BAND_MIN", str(1 << 20))) else 1,
+               path="streamed after level 0" if streamed else "row bands / one launch",
                ms_per_frame_median=round(med, 3), ms_min=round(min(ts), 3), ms_max=round(max(ts), 3),
                value=round(segments / (med * 1e-3) / 1e6, 3), unit="Mrays/s")
     if scene is not None:
-        prev = os.environ.get("RT_BANDS")
-        os.environ["RT_BANDS"] = "1"
+        env = {"RT_BANDS": "1", "RT_HOST_STREAM": "0"}
+        prev = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         try:
             one = rtamd.Context(device)
         finally:
-            if prev is None:
-                del os.environ["RT_BANDS"]
-            else:
-                os.environ["RT_BANDS"] = prev
+            for k, v in prev.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
         try:
             one.upload(scene)
             ts1, rgb1 = _host_frame_ms(one, cam, cfg, warm, reps)
@@ -641,12 +672,13 @@ def run_ranks(args, spec, scene, W, H, refmax, world, rank, local):
     sp = stream.cuda_stream
     sgs = [StripeGather(H, W, rank, world, args.stripe, dev) for _ in range(P)]
     sg = sgs[0]
+    cams = moving_cameras(W, H, args.steps + max(args.warmup, P))
 
-    def step(f, inflight):
+    def step(f, inflight, moving=False):
         i = f % inflight
         with torch.cuda.stream(streams[i]):
-            ctxs[i].trace_rows_device(cam, cfg, rank, world, args.stripe, sgs[i].local.data_ptr(),
-                                      streams[i].cuda_stream)
+            ctxs[i].trace_rows_device(cams[f % len(cams)] if moving else cam, cfg, rank, world, args.stripe,
+                                      sgs[i].local.data_ptr(), streams[i].cuda_stream)
             sgs[i].gather()        # the collective waits for this stream; this stream for it
 
     def sync():
@@ -716,10 +748,12 @@ def run_devices(args, spec, scene, W, H, refmax, n):
     streams = [torch.cuda.Stream(device=dev) for _ in range(P)]
     frames = [torch.zeros((H, W, 3), dtype=torch.float32, device=dev) for _ in range(P)]
     torch.cuda.synchronize(dev)
+    cams = moving_cameras(W, H, args.steps + max(args.warmup, P))
 
-    def step(f, inflight):
+    def step(f, inflight, moving=False):
         i = f % inflight
-        ctxs[i].trace_frame_device(cam, cfg, frames[i].data_ptr(), streams[i].cuda_stream)
+        ctxs[i].trace_frame_device(cams[f % len(cams)] if moving else cam, cfg, frames[i].data_ptr(),
+                                   streams[i].cuda_stream)
 
     def sync():
         for d in devs:
@@ -746,25 +780,38 @@ def run_devices(args, spec, scene, W, H, refmax, n):
     return out, 0
 
 
+YAW_STEP = 0.01                # rad per frame of the moving-camera run (Camera.rotate_h, src/view/camera.ts:90-93)
+
+
+def moving_cameras(W, H, n):
+    """n cameras of the bench view, each turned YAW_STEP further (rotate_h from the start angle), so
+    consecutive frames in flight see different pixels' worth of the scene, as an interactive view does."""
+    return [scenes.make_camera(W, H, init_h=math.pi / 6 + YAW_STEP * k) for k in range(n)]
+
+
 def timed_runs(args, P, step, sync, barrier, max_over_ranks):
-    def timed(inflight, steps, warmup):
+    """The timed frames: the moving camera first (step(f, inflight, moving=True)), then the static
+    camera with P frames in flight (the headline value), then one frame in flight.  The static runs
+    come last so that every slot ends with the static frame (frames_identical)."""
+    def timed(inflight, steps, warmup, moving=False):
         for f in range(warmup):
-            step(f, inflight)
+            step(f, inflight, moving)
         sync()
         barrier()
         sync()
         t0 = time.perf_counter()
         for f in range(steps):
-            step(f, inflight)
+            step(warmup + f, inflight, moving)
         sync()
         barrier()
         sync()
         return max_over_ranks(time.perf_counter() - t0)
 
     warm = max(args.warmup, P)     # every in-flight slot renders once before timing
+    el_moving = timed(P, args.steps, warm, moving=True)
     el = timed(P, args.steps, warm)
     el_serial = timed(1, args.steps, 1) if P > 1 else el
-    return dict(elapsed=el, elapsed_serial=el_serial, warmup_frames=warm)
+    return dict(elapsed=el, elapsed_serial=el_serial, elapsed_moving=el_moving, warmup_frames=warm)
 
 
 def main():
@@ -831,6 +878,14 @@ def report(args, res, spec, scene, W, H, refmax, build_s, deadline, reporter):
     value = tot["segments"] * steps / el / 1e6
     serial = dict(frames_in_flight=1, ms_per_frame=round(res["elapsed_serial"] / steps * 1e3, 4),
                   value=round(tot["segments"] * steps / res["elapsed_serial"] / 1e6, 3), unit="Mrays/s")
+    # the moving camera's frames differ in their segment counts: rays per second are the static
+    # frame's segments (the same pixels' worth of work within a few %), so this value is approximate
+    # to that extent; the frame rate is exact
+    moving = dict(frames_in_flight=res["P"], yaw_step_rad=YAW_STEP,
+                  ms_per_frame=round(res["elapsed_moving"] / steps * 1e3, 4),
+                  value=round(tot["segments"] * steps / res["elapsed_moving"] / 1e6, 3), unit="Mrays/s",
+                  note="each frame's camera turned %g rad further (rotate_h); value uses the static frame's "
+                       "segment count" % YAW_STEP)
 
     cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
     roofline = dict(bound=None, achieved=None, peak=None, unit=None, frac=None, traffic=None,
@@ -843,7 +898,8 @@ def report(args, res, spec, scene, W, H, refmax, build_s, deadline, reporter):
         "unit": "Mrays/s",
         "n_gpus": n_gpus,
         "steps": steps,
-        "warmup": res["warmup_frames"],
+        "warmup": args.warmup,
+        "warmup_effective": res["warmup_frames"],
         "ms_per_step": round(el / steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "strong",
@@ -858,6 +914,7 @@ def report(args, res, spec, scene, W, H, refmax, build_s, deadline, reporter):
                    "frames_identical": res["same"], "counters": tot, "scene_build_s": round(build_s, 3)},
         "roofline": roofline,
         "serial": serial,
+        "moving_camera": moving,
         "host_frame": res["host"],
         "js_frame": None,
         "cpu_baseline": None,
@@ -877,6 +934,8 @@ def report(args, res, spec, scene, W, H, refmax, build_s, deadline, reporter):
             kr = kernel_rooflines(dur, pmc, tot)
             roofline["kernels"] = kr
             roofline["kernel_ms_rocprof_sum"] = round(sum(dur.values()), 4)
+            hbm_counted = sum(v.get("hbm_bytes", 0) for v in kr.values())
+            roofline["hbm_8d"] = hbm_8d(tot, el / steps, hbm_counted)
             top = max(kr, key=lambda k: kr[k]["ms_per_frame"])
             t = kr[top]
             if "valu_issue_frac" in t or "hbm_frac" in t:

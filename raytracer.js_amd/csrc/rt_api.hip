@@ -149,9 +149,26 @@ struct rt_ctx {
     // automatic (the least K with at least l0_fill work items per resident wave of k_walk_first).
     // Default 1, off: measured slower at every part size (a wave's two walk phases cost their union)
     int l0_seg = 1;
+    int l0_bs = 64;                  // RT_L0_BS: threads per block of the level-0 walk + first-hit kernel
+    bool shade_hint = true;          // RT_SHADE_HINT=0: level 0's k_shade on the full persistent grid
+    int level_solo = 1;              // RT_LEVEL_SOLO=0: every level's five kernels, predicted no-ops on 8 blocks
+                                     // (2, tests: every bounce level as k_level)
     int l0_fill = 4;
     int64_t band_min = 1 << 20;      // RT_BAND_MIN: frames of fewer pixels run as one launch (256^2: 0.44 ms
                                      // one launch against 0.61 in 2 bands; 1080p and up gain, §5.14)
+    // Host-buffer frames on one GPU streamed after level 0 (trace_frame_stream): the
+    // level-0 result goes to the host while the bounce levels run, the pixels those write follow as a
+    // patch list.  RT_HOST_STREAM=0 restores the bands; frames of at least RT_STREAM_MIN pixels.
+    bool host_stream = true;
+    int64_t stream_min = 1 << 20;
+    int64_t late_cap = 0;            // RT_LATE_CAP > 0: the late list's capacity (tests: the overflow path)
+    // Host-buffer frames over several devices: each device copies its own stripes into the host buffer
+    // (trace_frame_parts_host; RT_HOST_DIRECT=0 restores the gather to devices[0] and one D2H)
+    bool host_direct = true;
+    hipStream_t copy = nullptr;      // dev[0]: the level-0 D2H (and the H2D of the previous values)
+    hipEvent_t ev_l0 = nullptr;      // level 0 shaded
+    DevBuf g_old, b_late;            // dev[0]: the previous ExposureBuffer values; the late-pixel list
+    int32_t *h_info = nullptr;       // pinned: fault flag, late-pixel count
     int n_band = 0;                  // band states initialised
     RtDevice band[RT_MAX_BANDS];     // streams and pass buffers of the bands (dev[0]'s GPU and scene)
     int32_t *h_fault = nullptr;      // pinned: each band's fault flag
@@ -245,7 +262,14 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_WF_LIST")) c->wf_list = atoll(e);
     if (const char *e = getenv("RT_L0_SEG")) c->l0_seg = atoi(e) <= 0 ? -1 : (atoi(e) == 1 ? 1 : pow2_at_most_64(std::min(atoi(e), 8)));
     if (const char *e = getenv("RT_L0_FILL")) c->l0_fill = std::max(0, atoi(e));
+    if (const char *e = getenv("RT_L0_BS")) c->l0_bs = atoi(e) == 64 ? 64 : 256;
+    if (const char *e = getenv("RT_SHADE_HINT")) c->shade_hint = atoi(e) != 0;
+    if (const char *e = getenv("RT_LEVEL_SOLO")) c->level_solo = std::min(2, std::max(0, atoi(e)));
     if (const char *e = getenv("RT_BAND_ORDER")) c->band_order = atoi(e) & 3;
+    if (const char *e = getenv("RT_HOST_STREAM")) c->host_stream = atoi(e) != 0;
+    if (const char *e = getenv("RT_STREAM_MIN")) c->stream_min = atoll(e) < 0 ? 0 : atoll(e);
+    if (const char *e = getenv("RT_LATE_CAP")) c->late_cap = atoll(e) < 0 ? 0 : atoll(e);
+    if (const char *e = getenv("RT_HOST_DIRECT")) c->host_direct = atoi(e) != 0;
     if (const char *e = getenv("RT_BANDS")) c->bands = atoi(e) < 1 ? 1 : (atoi(e) > RT_MAX_BANDS ? RT_MAX_BANDS : atoi(e));
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
     // parts on one GPU) gathers by device copies, as RT_CREATE_PEER_GATHER asks for.  RT_GATHER
@@ -325,8 +349,12 @@ extern "C" void rt_destroy(rt_ctx *c)
     rt_store_free(c->store);
     c->store = nullptr;
     (void)hipSetDevice(c->dev[0].device);
-    for (DevBuf *b : {&c->g_stack, &c->g_frame, &c->g_hit_e, &c->g_hit_n, &c->g_status, &c->b_stat, &c->b_walk})
+    for (DevBuf *b : {&c->g_stack, &c->g_frame, &c->g_hit_e, &c->g_hit_n, &c->g_status, &c->b_stat, &c->b_walk,
+                      &c->g_old, &c->b_late})
         b->release();
+    if (c->copy) (void)hipStreamSynchronize(c->copy), (void)hipStreamDestroy(c->copy);
+    if (c->ev_l0) (void)hipEventDestroy(c->ev_l0);
+    if (c->h_info) (void)hipHostFree(c->h_info);
     for (int b = 0; b < RT_MAX_BANDS; b++) release_device(c->band[b]);
     if (c->h_fault) (void)hipHostFree(c->h_fault);
     for (hipEvent_t e : c->band_walk)
@@ -594,6 +622,9 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.refill_always = c->refill_always;
     L.seg_max = c->seg_max;
     L.walk_first = (int64_t)d.scene.n_list <= c->wf_list;
+    L.l0_bs = c->l0_bs;
+    L.shade_hint = c->shade_hint && c->hints;
+    L.level_solo = c->level_solo == 2 ? 2 : (c->level_solo && c->hints);
     L.blend = cfg->col_weight != 1.0;
     if (c->split && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
@@ -979,6 +1010,198 @@ static int trace_frame_bands(rt_ctx *c, const rt_camera_desc *cam, const rt_conf
                                     "pixels from the first one in scan order on keep their previous value");
 }
 
+// rt_trace_frame on one GPU without counters, streamed.  Most rays of a frame end at
+// level 0 (config 3: 99 %), so once level 0 is shaded the frame buffer holds nearly every final pixel:
+// a copy stream sends it to the host while the bounce levels run, and the pixels those levels (and
+// k_cont) write afterwards come back as a compact list (RtLate) patched over the copy.  The previous
+// ExposureBuffer values travel to the device first (H2D, overlapping level 0), so that a frame with a
+// reference throw still leaves the reference's partial frame (§3.3): the host restores them from there.
+// *done = false when the frame cannot stream (the fused kernel runs it): the caller takes another path.
+static int trace_frame_stream(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,
+                              int32_t *hit_entity, int32_t *hit_node, uint8_t *status, bool *done)
+{
+    RtDevice &d0 = c->dev[0];
+    const int W = cam->width, H = cam->height;
+    const size_t P = (size_t)W * (size_t)H;
+    const bool ids = hit_entity || hit_node, blend = cfg->col_weight != 1.0;
+    *done = false;
+    RtLaunch L;
+    int r;
+    if ((r = prepare(c, d0, cam, cfg, 0, 1, H, WANT_STATUS | (ids ? WANT_IDS : 0), L)) != RT_OK) return r;
+    if (!L.cand) return RT_OK;                                          // fused: not streamable
+    // the late list: twice the pixels a recent frame left after level 0 (queued to level 1 or k_cont),
+    // at least 2^16; more than that falls back to copying the whole frame again
+    const int32_t *h = L.ctr_hint;
+    const long long late_hint = h && h[4] >= 0 && h[0] >= 0 ? (long long)h[4] + h[0] : -1;
+    const long long cap = c->late_cap > 0 ? c->late_cap
+                        : std::min<long long>((long long)P, late_hint >= 0 ? std::max(1ll << 16, 2 * late_hint)
+                                                                           : std::max<long long>(1 << 16, P / 4));
+    if ((r = d0.b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
+    if ((r = c->g_old.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
+    if ((r = c->b_late.ensure(sizeof(RtLate) * (size_t)cap + 16)) != RT_OK) return r;
+    if (!c->copy) HIP_TRY(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+    if (!c->ev_l0) HIP_TRY(hipEventCreateWithFlags(&c->ev_l0, hipEventDisableTiming));
+    if (!c->h_info) HIP_TRY(hipHostMalloc((void **)&c->h_info, 2 * sizeof(int32_t), hipHostMallocDefault));
+    float *f_rgb = (float *)d0.b_rgb.p, *old = (float *)c->g_old.p;
+    RtLate *late = (RtLate *)c->b_late.p;
+    int32_t *late_n = (int32_t *)(late + cap);
+    L.rgb = f_rgb;
+    L.late = late;
+    L.late_n = late_n;
+    L.late_cap = (int32_t)cap;
+    L.l0_done = c->ev_l0;
+    hipStream_t S = d0.stream, Cs = c->copy;
+    if (blend) {                                  // the blend reads the previous values on the device
+        HIP_TRY(hipMemcpyAsync(f_rgb, rgb_inout, sizeof(float) * 3 * P, hipMemcpyHostToDevice, S));
+        HIP_TRY(hipMemcpyAsync(old, f_rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToDevice, S));
+    }
+    HIP_TRY(hipMemsetAsync(d0.b_fault.p, 0, sizeof(int), S));
+    HIP_TRY(hipMemsetAsync(late_n, 0, sizeof(int32_t), S));
+    hipEvent_t *ev = next_events(d0);
+    if ((r = rt_launch_frame(L, S, ev[0], ev[1])) != RT_OK) return r;
+    HIP_TRY(hipMemcpyAsync(&c->h_info[0], d0.b_fault.p, sizeof(int32_t), hipMemcpyDeviceToHost, S));
+    HIP_TRY(hipMemcpyAsync(&c->h_info[1], late_n, sizeof(int32_t), hipMemcpyDeviceToHost, S));
+    HIP_TRY(hipEventRecord(d0.sync, S));
+    // the copy stream: the previous values up (they are read before the level-0 result overwrites the
+    // host buffer: same stream), then, once level 0 is shaded, the frame down
+    if (!blend) HIP_TRY(hipMemcpyAsync(old, rgb_inout, sizeof(float) * 3 * P, hipMemcpyHostToDevice, Cs));
+    HIP_TRY(hipStreamWaitEvent(Cs, c->ev_l0, 0));
+    HIP_TRY(hipMemcpyAsync(rgb_inout, f_rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost, Cs));
+    if (hit_entity) HIP_TRY(hipMemcpyAsync(hit_entity, L.hit_entity, sizeof(int32_t) * P, hipMemcpyDeviceToHost, Cs));
+    if (hit_node) HIP_TRY(hipMemcpyAsync(hit_node, L.hit_node, sizeof(int32_t) * P, hipMemcpyDeviceToHost, Cs));
+    if (status) HIP_TRY(hipMemcpyAsync(status, L.status, P, hipMemcpyDeviceToHost, Cs));
+    HIP_TRY(hipEventSynchronize(d0.sync));
+    HIP_TRY(hipStreamSynchronize(Cs));
+    *done = true;
+    const int fault = c->h_info[0], n_late = c->h_info[1];
+    if (!fault) {
+        if (n_late <= cap) {
+            std::vector<RtLate> lt((size_t)n_late);
+            if (n_late) HIP_TRY(hipMemcpy(lt.data(), late, sizeof(RtLate) * (size_t)n_late, hipMemcpyDeviceToHost));
+            for (const RtLate &e : lt) {
+                float *px = rgb_inout + 3 * (size_t)e.pix;
+                px[0] = e.rgb[0]; px[1] = e.rgb[1]; px[2] = e.rgb[2];
+                if (hit_entity) hit_entity[e.pix] = e.hit_e;
+                if (hit_node) hit_node[e.pix] = e.hit_n;
+                if (status) status[e.pix] = (uint8_t)e.status;
+            }
+        } else {                                  // the list overflowed: the whole final frame again
+            HIP_TRY(hipMemcpy(rgb_inout, f_rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost));
+            if (hit_entity) HIP_TRY(hipMemcpy(hit_entity, L.hit_entity, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
+            if (hit_node) HIP_TRY(hipMemcpy(hit_node, L.hit_node, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
+            if (status) HIP_TRY(hipMemcpy(status, L.status, P, hipMemcpyDeviceToHost));
+        }
+        return RT_OK;
+    }
+    // a throwing frame: the whole final frame, the previous values back, then the reference's partial frame
+    std::vector<uint8_t> st_tmp;
+    uint8_t *st_host = status;
+    if (!st_host) {
+        st_tmp.resize(P);
+        st_host = st_tmp.data();
+    }
+    std::vector<float> fresh(3 * P);
+    HIP_TRY(hipMemcpy(fresh.data(), f_rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(st_host, L.status, P, hipMemcpyDeviceToHost));
+    if (hit_entity) HIP_TRY(hipMemcpy(hit_entity, L.hit_entity, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
+    if (hit_node) HIP_TRY(hipMemcpy(hit_node, L.hit_node, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(rgb_inout, old, sizeof(float) * 3 * P, hipMemcpyDeviceToHost));
+    keep_after_first_throw(rgb_inout, fresh.data(), st_host, W, H);
+    return rt_set_error(RT_E_FAULT, "a ray reached a state where the reference throws (status 2/3 pixels); "
+                                    "pixels from the first one in scan order on keep their previous value");
+}
+
+// The stripes of part k of N between its part buffer (rows in part order, row_bytes each) and a
+// frame-layout host buffer: one 2D copy for its full stripes (pitch N stripes) and one for a partial
+// last stripe of the frame.  to_host: D2H, else H2D.
+static int copy_part_stripes(void *host, void *part, int H, int k, int N, int stripe, size_t row_bytes, bool to_host,
+                             hipStream_t st)
+{
+    const int n_stripes = (H + stripe - 1) / stripe;
+    int n_full = 0, last_rows = 0;
+    for (int s = k; s < n_stripes; s += N) {
+        const int rows = std::min(stripe, H - s * stripe);
+        if (rows == stripe) n_full++;
+        else last_rows = rows;                                    // only the frame's last stripe is partial
+    }
+    uint8_t *h = (uint8_t *)host + (size_t)k * stripe * row_bytes;
+    uint8_t *p = (uint8_t *)part;
+    const size_t sb = (size_t)stripe * row_bytes, hp = (size_t)N * sb;
+    if (n_full > 0) {
+        if (to_host) HIP_TRY(hipMemcpy2DAsync(h, hp, p, sb, sb, (size_t)n_full, hipMemcpyDeviceToHost, st));
+        else HIP_TRY(hipMemcpy2DAsync(p, sb, h, hp, sb, (size_t)n_full, hipMemcpyHostToDevice, st));
+    }
+    if (last_rows > 0) {
+        const size_t nb = (size_t)last_rows * row_bytes;
+        uint8_t *hl = h + (size_t)n_full * hp, *pl = p + (size_t)n_full * sb;
+        if (to_host) HIP_TRY(hipMemcpyAsync(hl, pl, nb, hipMemcpyDeviceToHost, st));
+        else HIP_TRY(hipMemcpyAsync(pl, hl, nb, hipMemcpyHostToDevice, st));
+    }
+    return RT_OK;
+}
+
+// rt_trace_frame over several devices without counters: every device traces its part
+// into its own buffers, the fault flags come back, and then each device copies its part's stripes
+// straight into the host buffers over its own link, all devices at once: no gather to devices[0] and
+// no single full-frame D2H.  A blend first sends each device its part of the current frame the same
+// way.  A throwing frame is assembled in a temporary buffer (the reference's partial frame, §3.3).
+static int trace_frame_parts_host(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,
+                                  int32_t *hit_entity, int32_t *hit_node, uint8_t *status)
+{
+    const int N = c->n_dev, H = cam->height, W = cam->width, stripe = c->stripe;
+    const size_t P = (size_t)W * (size_t)H;
+    const bool blend = cfg->col_weight != 1.0;
+    const bool ids = hit_entity || hit_node;
+    RtLaunch L[RT_MAX_DEVICES];
+    int r;
+    for (int k = 0; k < N; k++) {
+        RtDevice &d = c->dev[k];
+        if ((r = use_device(d)) != RT_OK) return r;
+        if ((r = prepare(c, d, cam, cfg, k, N, stripe, WANT_STATUS | (ids ? WANT_IDS : 0), L[k])) != RT_OK) return r;
+        const size_t PS = (size_t)L[k].rows * (size_t)W;
+        if ((r = d.b_rgb.ensure(sizeof(float) * 3 * (PS ? PS : 1))) != RT_OK) return r;
+        L[k].rgb = (float *)d.b_rgb.p;
+        if (blend && PS && (r = copy_part_stripes(rgb_inout, L[k].rgb, H, k, N, stripe, (size_t)W * 12, false, d.stream)))
+            return r;
+        HIP_TRY(hipMemsetAsync(d.b_fault.p, 0, sizeof(int), d.stream));
+        hipEvent_t *ev = next_events(d);
+        if ((r = rt_launch_frame(L[k], d.stream, ev[0], ev[1])) != RT_OK) return r;
+    }
+    int fault = 0;
+    if ((r = finish(c, 0, nullptr, std::chrono::steady_clock::now(), &fault)) != RT_OK) return r;
+    std::vector<float> fresh;
+    std::vector<uint8_t> st_tmp;
+    float *rgb_dst = rgb_inout;
+    uint8_t *st_dst = status;
+    if (fault) {
+        fresh.resize(3 * P);
+        rgb_dst = fresh.data();
+        if (!st_dst) {
+            st_tmp.resize(P);
+            st_dst = st_tmp.data();
+        }
+    }
+    for (int k = 0; k < N; k++) {
+        RtDevice &d = c->dev[k];
+        if (!L[k].rows) continue;
+        if ((r = use_device(d)) != RT_OK) return r;
+        if ((r = copy_part_stripes(rgb_dst, L[k].rgb, H, k, N, stripe, (size_t)W * 12, true, d.stream))) return r;
+        if (hit_entity && (r = copy_part_stripes(hit_entity, L[k].hit_entity, H, k, N, stripe, (size_t)W * 4, true, d.stream)))
+            return r;
+        if (hit_node && (r = copy_part_stripes(hit_node, L[k].hit_node, H, k, N, stripe, (size_t)W * 4, true, d.stream)))
+            return r;
+        if (st_dst && (r = copy_part_stripes(st_dst, L[k].status, H, k, N, stripe, (size_t)W, true, d.stream))) return r;
+    }
+    for (int k = 0; k < N; k++) {
+        HIP_TRY(hipSetDevice(c->dev[k].device));
+        HIP_TRY(hipStreamSynchronize(c->dev[k].stream));
+    }
+    if (!fault) return RT_OK;
+    keep_after_first_throw(rgb_inout, fresh.data(), st_dst, W, H);
+    return rt_set_error(RT_E_FAULT, "a ray reached a state where the reference throws (status 2/3 pixels); "
+                                    "pixels from the first one in scan order on keep their previous value");
+}
+
 extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,
                               int32_t *hit_entity, int32_t *hit_node, uint8_t *status, rt_stats *stats)
 {
@@ -994,8 +1217,15 @@ extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     const size_t P = (size_t)W * (size_t)H;
     const bool blend = cfg->col_weight != 1.0;
     FrameOut o = {};
+    if (c->gather == RT_GATHER_NONE && !stats && c->host_stream && c->split && (int64_t)P >= c->stream_min) {
+        bool done = false;
+        r = trace_frame_stream(c, cam, cfg, rgb_inout, hit_entity, hit_node, status, &done);
+        if (r != RT_OK || done) return r;
+    }
     if (c->gather == RT_GATHER_NONE && !stats && c->bands > 1 && c->split && H >= 16 && (int64_t)P >= c->band_min)
         return trace_frame_bands(c, cam, cfg, rgb_inout, hit_entity, hit_node, status, c->bands);
+    if (c->gather != RT_GATHER_NONE && !stats && c->host_direct)
+        return trace_frame_parts_host(c, cam, cfg, rgb_inout, hit_entity, hit_node, status);
     if (c->gather == RT_GATHER_NONE) {
         RtLaunch L;
         // per-pixel status always: it locates the first throwing pixel of a faulting frame

@@ -105,6 +105,15 @@ struct alignas(16) RtCont {
 };
 static_assert(sizeof(RtCont) == 112, "RtCont must stay 112 bytes");
 
+// A pixel written after level 0 (bounce levels, k_cont) of a frame whose level-0 result already went
+// to the host (rt_api.hip trace_frame_stream): the host patches these over that copy.
+struct RtLate {
+    int32_t pix;
+    float rgb[3];
+    int32_t hit_e, hit_n, status, pad;
+};
+static_assert(sizeof(RtLate) == 32, "RtLate must stay 32 bytes");
+
 // Per-frame state computed on the device by the setup kernel.
 struct RtFrameSetup {
     int32_t start_tree;   // node_at_pos(otree, camera.pos) → tree (-1: null)
@@ -215,6 +224,17 @@ struct RtLaunch {
     int32_t walk_first;                         // level 0 as one walk + first-hit kernel (k_walk_first; §5.18)
     int32_t l0_seg;                             // > 1: level 0 with K segments per primary ray (k_walk_first_seg; §5.20)
     int32_t tl;                                 // RT_TL builds: this launch's timeline record (-1: none)
+    int32_t l0_bs;                              // threads per block of k_walk_first (RT_L0_BS: 64 or 256)
+    int32_t shade_hint;                         // level 0's k_shade grid from a recent frame's queue (RT_SHADE_HINT)
+    int32_t level_solo;                         // narrow predicted levels as one k_level launch (RT_LEVEL_SOLO)
+    // host frames streamed after level 0 (rt_api.hip trace_frame_stream): launches with late_write set
+    // (bounce levels, k_cont) also append every pixel they write to late[] (count *late_n, at most
+    // late_cap kept); l0_done (hipEvent_t) is recorded once level 0 is shaded
+    RtLate *late;
+    int32_t *late_n;
+    int32_t late_cap;
+    int32_t late_write;
+    void *l0_done;
     const int32_t *ctr_hint;                    // host snapshot of a recent frame's ctr (-1: none yet), or null
     int32_t *ctr_out;                           // pinned: this frame's ctr is copied here at its end (or null)
     void *ctr_done;                             // hipEvent_t recorded after that copy

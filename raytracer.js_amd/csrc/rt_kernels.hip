@@ -42,16 +42,24 @@ constexpr int STEP_CAP = 1 << 24;                // per-walk loop bound: every l
 #endif
 #if RT_TL
 enum { RT_TL_MAX = 1 << 16 };
-__device__ unsigned long long g_tl[RT_TL_MAX][2];
+// per launch: first wave start, last wave end, summed wave lifetimes, waves
+__device__ unsigned long long g_tl[RT_TL_MAX][4];
 struct TlScope {
     int id;
+    unsigned long long t0;
     __device__ explicit TlScope(int i) : id(i)
     {
-        if (id >= 0 && (threadIdx.x & 63) == 0) atomicMin(&g_tl[id][0], (unsigned long long)wall_clock64());
+        t0 = wall_clock64();
+        if (id >= 0 && (threadIdx.x & 63) == 0) atomicMin(&g_tl[id][0], t0);
     }
     __device__ ~TlScope()
     {
-        if (id >= 0 && (threadIdx.x & 63) == 0) atomicMax(&g_tl[id][1], (unsigned long long)wall_clock64());
+        const unsigned long long t1 = wall_clock64();
+        if (id >= 0 && (threadIdx.x & 63) == 0) {
+            atomicMax(&g_tl[id][1], t1);
+            atomicAdd(&g_tl[id][2], t1 - t0);
+            atomicAdd(&g_tl[id][3], 1ull);
+        }
     }
 };
 #define TL_SCOPE(i) TlScope tl_scope_(i)
@@ -1224,16 +1232,23 @@ __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_des
         const double sv = top ? cam.scan_v[1] : -cam.scan_v[1];
         if (!top) rotate_1(f, u, c, sv);
         const int steps = top ? y - (H >> 1) : (H >> 1) - 1 - y;
+        // a single-wave dependent chain (the frame's critical path is H/2 + W/2 of these steps):
+        // unrolled, so that a step is its four multiplies and two adds
+#pragma unroll 4
         for (int k = 0; k < steps; k++) rotate_1(f, u, c, sv);
     }
     // iter_h(W>>1, W, y, rot_scan_h_v, fr_v, 1, false) / iter_h((W>>1)-1, -1, y, counter, fr_v, -1, true)
     const double c = cam.scan_h[0], sh = right ? cam.scan_h[1] : -cam.scan_h[1];
     double l = cam.lf[i];
     if (!right) rotate_1(f, l, c, sh);
-    const int from = right ? (W >> 1) : (W >> 1) - 1, to = right ? W : -1, inc = right ? 1 : -1;
-    double *plane = dirs + (size_t)i * (size_t)rows * (size_t)W;
-    for (int x = from; x != to; x += inc) {
-        plane[(size_t)x * (size_t)rows + (size_t)lr] = f;
+    const int from = right ? (W >> 1) : (W >> 1) - 1, inc = right ? 1 : -1;
+    double *p = dirs + (size_t)i * (size_t)rows * (size_t)W + (size_t)from * (size_t)rows + (size_t)lr;
+    const ptrdiff_t step = (ptrdiff_t)inc * (ptrdiff_t)rows;
+    const int n = right ? W - from : from + 1;
+#pragma unroll 4
+    for (int k = 0; k < n; k++) {
+        *p = f;
+        p += step;
         rotate_1(f, l, c, sh);
     }
 }
@@ -1543,10 +1558,23 @@ __device__ __forceinline__ void write_pixel(const RtLaunch &L, size_t pix, const
         v += old * (1 - wgt);
         px[k] = (float)v;
     }
+    const int hn = R.hit_node >= 0 ? L.scene.node_dfs[R.hit_node] : R.hit_node;
     if (L.hit_entity) L.hit_entity[pix] = R.hit_ent;
-    if (L.hit_node) L.hit_node[pix] = R.hit_node >= 0 ? L.scene.node_dfs[R.hit_node] : R.hit_node;
+    if (L.hit_node) L.hit_node[pix] = hn;
     if (L.status) L.status[pix] = (uint8_t)R.status;
     if (R.status >= ST_FAULT && L.fault) atomicOr(L.fault, 1);
+    if (L.late_write && L.late) {                 // after level 0 of a streamed host frame: the patch list
+        const int k = wave_reserve(L.late_n);
+        if (k < L.late_cap) {
+            RtLate &e = L.late[k];
+            e.pix = (int32_t)pix;
+            e.rgb[0] = px[0]; e.rgb[1] = px[1]; e.rgb[2] = px[2];
+            e.hit_e = R.hit_ent;
+            e.hit_n = hn;
+            e.status = R.status;
+            e.pad = 0;
+        }
+    }
 }
 
 // ---- work distribution ------------------------------------------------------------------------------------
@@ -1770,11 +1798,11 @@ struct SegLane {
     int K, rpw, j, base, n_rays;
     double frac;
 };
-__device__ __forceinline__ SegLane seg_lane(const RtLaunch &L)
+__device__ __forceinline__ SegLane seg_lane(const RtLaunch &L, int K)
 {
     SegLane g;
     const int lane = threadIdx.x & 63;
-    g.K = L.seg;
+    g.K = K;
     g.rpw = 64 / g.K;                            // rays per wave
     g.j = lane & (g.K - 1);
     g.base = lane & ~(g.K - 1);
@@ -1902,12 +1930,11 @@ __device__ __forceinline__ bool seg_shaded(const RtLaunch &L)
 {
     return RT_SEG_FUSED && RT_SEG_SHADE && L.level >= 1 && seg_mode(L) && *lvl_ctr(L, L.level - 1) <= RT_SEG_SHADE_MAX;
 }
-template <int MINW, bool SHADE>
-__global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
+// A segmented level's items: walk, scan and (SHADE) shading per work item, until the level's queue of
+// items is empty (k_seg, k_level).
+template <bool SHADE>
+__device__ __forceinline__ void seg_level(const RtLaunch &L, int K)
 {
-    TL_SCOPE(L.tl);
-    if (!seg_mode(L) || seg_shaded(L) != SHADE) return;     // the other instantiation takes this level
-    stage_top(L.scene);
     const int lane = threadIdx.x & 63;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const RtDevScene &S = L.scene;
@@ -1915,7 +1942,7 @@ __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
     const bool fault = L.setup->fault != 0;
     const RtFrameSetup F = *L.setup;
     const RayQueues Q = {L.queue[L.level & 1], lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
-    const SegLane g = seg_lane(L);
+    const SegLane g = seg_lane(L, K);
     const int items = (g.n_rays + g.rpw - 1) / g.rpw;
     for (;;) {
         int t_end;
@@ -1941,6 +1968,15 @@ __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
     }
 }
 
+template <int MINW, bool SHADE>
+__global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
+{
+    TL_SCOPE(L.tl);
+    if (!seg_mode(L) || seg_shaded(L) != SHADE) return;     // the other instantiation takes this level
+    stage_top(L.scene);
+    seg_level<SHADE>(L, L.seg);
+}
+
 // The two passes apart (RT_SEG_FUSED = 0).
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
@@ -1951,7 +1987,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
     const int lane = threadIdx.x & 63;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
-    const SegLane g = seg_lane(L);
+    const SegLane g = seg_lane(L, L.seg);
     const int items = (g.n_rays + g.rpw - 1) / g.rpw;
     for (;;) {
         int t_end;
@@ -1970,7 +2006,7 @@ __global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const bool fault = L.setup->fault != 0;
-    const SegLane g = seg_lane(L);
+    const SegLane g = seg_lane(L, L.seg);
     const int items = (g.n_rays + g.rpw - 1) / g.rpw;
     for (;;) {
         int t_end;
@@ -2296,8 +2332,8 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
 // their first-hit tests at once, from lists it has just written (cache-resident), so a CU interleaves
 // walking waves (VALU-bound) with testing waves (latency-bound) instead of running the two passes
 // one after the other.  Same walk, same lists, same tests: identical results.
-template <int MINW>
-__global__ void __launch_bounds__(256, MINW) k_walk_first(RtLaunch L)
+template <int MINW, int BS = 256>
+__global__ void __launch_bounds__(BS, MINW) k_walk_first(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
@@ -2543,6 +2579,20 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
     }
 }
 
+// A narrow bounce level as ONE launch (L.level_solo): where a recent frame predicts a
+// segmented level that k_seg shades, the host launches this kernel alone instead of the level's five
+// kernels of which four return at once (k_walk, k_seg<false>, k_first, k_shade; in flight each such
+// launch held its frame's stream ~0.1 ms).  A wrong prediction stays correct: a level that is not
+// segmentable on the device runs as segmented walks of one segment per ray (K = 1: each lane walks
+// its ray from the origin, then scans and shades it), the same code with the same registers.
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_level(RtLaunch L)
+{
+    TL_SCOPE(L.tl);
+    stage_top(L.scene);
+    seg_level<true>(L, seg_mode(L) ? L.seg : 1);
+}
+
 template <bool INCL_UNDEF>
 __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, double dx, double dy, double dz,
                              int max_out, int32_t *out_tree, int32_t *out_oct, int32_t *n_out)
@@ -2578,6 +2628,10 @@ __global__ void k_debug_walk(RtDevScene S, double ox, double oy, double oz, doub
 // makes an over-estimate harmless (late blocks find the queue empty).  The CU count and each
 // kernel's blocks per CU are queried once (all devices of a context are MI355X): one host thread
 // issues the launches of up to 8 GPUs, so a launch is only the launch.
+#ifndef RT_NO_OP_BLOCKS
+#define RT_NO_OP_BLOCKS 8              // grid of a bounce-level kernel predicted to return at once (0: full)
+#endif
+
 // RT_TL builds: launch id -> (kernel expression, stream); ids wrap at RT_TL_MAX (the reader resets)
 #if RT_TL
 static std::mutex g_tl_mu;
@@ -2593,9 +2647,14 @@ static int tl_next(const void *name, hipStream_t st)
 static int tl_next(const void *, hipStream_t) { return -1; }
 #endif
 
+// bs: threads per block.  A grid cap (max_blocks) counts 256-thread blocks whatever bs is.
 static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const RtLaunch &L0, int max_blocks = 0,
-                              size_t lds = 0)
+                              size_t lds = 0, int bs = 256)
 {
+    // RT_SKIP_NOOP=1 (timing experiments only: a wrong prediction drops a level's work) launches
+    // nothing where the grid hints predict an immediate return
+    static const bool skip_noop = getenv("RT_SKIP_NOOP") && atoi(getenv("RT_SKIP_NOOP")) != 0;
+    if (skip_noop && max_blocks == RT_NO_OP_BLOCKS) return;
     RtLaunch L = L0;
     L.tl = tl_next(reinterpret_cast<const void *>(kernel), st);
     static std::atomic<int> cus{0};
@@ -2616,18 +2675,15 @@ static void launch_persistent(void (*kernel)(RtLaunch), hipStream_t st, const Rt
         for (const auto &e : per_kernel)
             if (e.first == key) per = e.second;
         if (!per) {
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kp, 256, lds) != hipSuccess || per < 1) per = 1;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kp, bs, lds) != hipSuccess || per < 1) per = 1;
             per_kernel.emplace_back(key, per);
         }
     }
     int nb = n_cu * per;
-    if (max_blocks > 0 && nb > max_blocks) nb = max_blocks;
-    hipLaunchKernelGGL(kernel, dim3(nb), dim3(256), lds, st, L);
+    if (max_blocks > 0 && nb > max_blocks * (256 / bs)) nb = max_blocks * (256 / bs);
+    hipLaunchKernelGGL(kernel, dim3(nb), dim3(bs), lds, st, L);
 }
 
-#ifndef RT_NO_OP_BLOCKS
-#define RT_NO_OP_BLOCKS 8              // grid of a bounce-level kernel predicted to return at once (0: full)
-#endif
 // Grid of a bounce-level pass (or k_cont).  Persistent passes are correct at any grid size: waves
 // claim work until the level's queue is empty.  A level of a small part holds a few thousand rays,
 // and launching the full persistent grid for it costs more in block dispatch than the work (8-part
@@ -2679,6 +2735,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
         for (int lv = 0; lv <= levels; lv++) {
             RtLaunch Lv = L;
             Lv.level = lv;
+            Lv.late_write = lv >= 1;
             Lv.last_level = lv == levels && levels < want;
             const int32_t hint = lv >= 1 && L.ctr_hint ? L.ctr_hint[4 + RT_CTR_LEVEL * (lv - 1)] : -1;
             const int mb = lv >= 1 ? level_blocks(L, hint) : L.l0_blocks;
@@ -2692,6 +2749,11 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             // costs time, and a small part's frame no longer dispatches full grids that do nothing.
             int mb_plain = mb, mb_seg = mb, mb_refill = mb, mb_first = mb, mb_first_seg = mb, mb_shade = mb;
             int mb_seg_shade = mb, mb_seg_wide = mb;
+            if (lv == 0 && L.shade_hint && L.ctr_hint && L.ctr_hint[5] >= 0) {
+                // level 0's shading queue of a recent frame (shade_n): 64 rays per work item, 2x headroom
+                const long long items = ((long long)L.ctr_hint[5] + 63) / 64;
+                mb_shade = (int)std::min<long long>(std::max<long long>(8, (2 * items + 3) / 4), 1 << 20);
+            }
             if (lv >= 1 && hint >= 0 && RT_NO_OP_BLOCKS > 0) {
                 const long long P = (long long)L.rows * (long long)L.cam.width;
                 const bool seg = L.seg > 1 && (L.seg_max <= 0 || hint <= L.seg_max) && (long long)hint * L.seg <= P;
@@ -2706,12 +2768,29 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
                 if (refill) mb_plain = RT_NO_OP_BLOCKS;
                 else mb_refill = RT_NO_OP_BLOCKS;
             }
+            // a narrow level predicted segmented and shaded by k_seg: one k_level launch (k_cont folded
+            // into the last level's when a recent frame had nothing for it)
+            // (level_solo 2, tests: every bounce level through k_level)
+            const bool solo = lv >= 1 && (L.level_solo == 2 || (L.level_solo && hint >= 0 &&
+                                                                 mb_shade == RT_NO_OP_BLOCKS && RT_NO_OP_BLOCKS > 0));
+            if (solo) {
+                RtLaunch Lw = Lv;
+                Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
+                launch_persistent(k_level<2>, st, Lw, mb_seg_shade, sizeof(RtNode) * (size_t)Lw.scene.n_lds);
+                HIP_TRY(hipGetLastError());
+                continue;
+            }
             if (lv == 0 && walk_wait) HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)walk_wait, 0));
             RtLaunch Lw = Lv;                         // the walk kernels read the upper levels from LDS
             Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
             const size_t lds = sizeof(RtNode) * (size_t)Lw.scene.n_lds;
             if (L.l0_seg > 1 && lv == 0) launch_persistent(k_walk_first_seg<4>, st, Lw, mb, lds);
-            else if (L.walk_first && lv == 0) launch_persistent(k_walk_first<4>, st, Lw, mb, lds);
+            else if (L.walk_first && lv == 0) {
+                // one wave per block: a part of an 8-GPU frame gives each wave about one tile, and a
+                // 4-wave block would hold its SIMD slots until its slowest tile ends
+                if (L.l0_bs == 64) launch_persistent(k_walk_first<4, 64>, st, Lw, mb, lds, 64);
+                else launch_persistent(k_walk_first<4>, st, Lw, mb, lds);
+            }
             else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb_plain, lds);
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
@@ -2730,10 +2809,13 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             if (lv >= 1 && L.seg > 1 && !RT_SEG_FUSED) launch_persistent(k_first_seg<4>, st, Lv, mb_first_seg);
             launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv, mb_shade);
             HIP_TRY(hipGetLastError());
+            if (lv == 0 && L.l0_done) HIP_TRY(hipEventRecord((hipEvent_t)L.l0_done, st));
         }
         // k_cont: a recent frame with no ray left over predicts none now (NO_OP_BLOCKS still finish any)
         const int32_t cont_hint = L.ctr_hint ? L.ctr_hint[0] : -1;
-        launch_persistent(k_cont<3>, st, L,
+        RtLaunch Lc = L;
+        Lc.late_write = 1;
+        launch_persistent(k_cont<3>, st, Lc,
                           cont_hint == 0 && RT_NO_OP_BLOCKS > 0 && L.lv_blocks <= 0 ? RT_NO_OP_BLOCKS : level_blocks(L, cont_hint));
         // this frame's counters come back for the next frames' grid hints (any recent frame will do)
         if (L.ctr_out) {
@@ -2760,10 +2842,11 @@ int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[
     return RT_OK;
 }
 
-// RT_TL builds: the launches recorded since the last reset — start / end (100 MHz wall clock) of each,
+// RT_TL builds: the launches recorded since the last reset — first wave start, last wave end, summed
+// wave lifetimes and wave count (100 MHz wall clock) of each,
 // its kernel expression (up to 63 characters) and stream — then (reset) a new timeline.  Returns the
 // count, or RT_E_UNSUPPORTED in production builds.
-extern "C" int rt_debug_timeline(int32_t max, unsigned long long *start_end, char *names, unsigned long long *streams,
+extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *names, unsigned long long *streams,
                                  int32_t reset)
 {
 #if RT_TL
@@ -2771,24 +2854,25 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *start_end, cha
     const int n = (int)std::min<size_t>(g_tl_host.size(), (size_t)std::max(0, max));
     if (n > 0) {
         if (hipDeviceSynchronize() != hipSuccess) return RT_E_HIP;
-        std::vector<unsigned long long> v(2 * (size_t)n);
-        if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_tl), sizeof(unsigned long long) * 2 * n) != hipSuccess)
+        std::vector<unsigned long long> v(4 * (size_t)n);
+        if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_tl), sizeof(unsigned long long) * 4 * n) != hipSuccess)
             return RT_E_HIP;
         static const std::pair<const void *, const char *> known[] = {
             {(const void *)k_frame_start, "k_frame_start"}, {(const void *)k_trace<true, 2>, "k_trace"},
             {(const void *)k_trace<false, 2>, "k_trace"}, {(const void *)k_trace<false, 3>, "k_trace"},
             {(const void *)k_trace<false, 4>, "k_trace"}, {(const void *)k_walk_first<4>, "k_walk_first"},
+            {(const void *)k_walk_first<4, 64>, "k_walk_first"},
             {(const void *)k_walk_first_seg<4>, "k_walk_first_seg"}, {(const void *)k_walk<3>, "k_walk"},
             {(const void *)k_walk<4>, "k_walk"}, {(const void *)k_walk<5>, "k_walk"},
             {(const void *)k_seg<2, false>, "k_seg_wide"}, {(const void *)k_seg<2, true>, "k_seg"},
+            {(const void *)k_level<2>, "k_level"},
             {(const void *)k_walk_seg<2>, "k_walk_seg"}, {(const void *)k_walk_refill<RT_REFILL_OCC>, "k_walk_refill"},
             {(const void *)k_first<4>, "k_first"}, {(const void *)k_first<6>, "k_first"}, {(const void *)k_first<8>, "k_first"},
             {(const void *)k_first_refill<6>, "k_first_refill"}, {(const void *)k_first_seg<4>, "k_first_seg"},
             {(const void *)k_shade<3>, "k_shade"}, {(const void *)k_shade<4>, "k_shade"}, {(const void *)k_shade<5>, "k_shade"},
             {(const void *)k_cont<3>, "k_cont"}};
         for (int i = 0; i < n; i++) {
-            start_end[2 * i] = v[2 * i];
-            start_end[2 * i + 1] = v[2 * i + 1];
+            for (int q = 0; q < 4; q++) rec4[4 * i + q] = v[4 * i + q];
             const char *nm = "?";
             for (const auto &k : known)
                 if (k.first == g_tl_host[i].first) nm = k.second;
@@ -2798,15 +2882,15 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *start_end, cha
     }
     if (reset) {
         if (hipDeviceSynchronize() != hipSuccess) return RT_E_HIP;
-        std::vector<unsigned long long> init(2 * (size_t)RT_TL_MAX);
-        for (size_t i = 0; i < init.size(); i += 2) { init[i] = ~0ull; init[i + 1] = 0; }
+        std::vector<unsigned long long> init(4 * (size_t)RT_TL_MAX, 0ull);
+        for (size_t i = 0; i < init.size(); i += 4) init[i] = ~0ull;
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_tl), init.data(), sizeof(unsigned long long) * init.size()) != hipSuccess)
             return RT_E_HIP;
         g_tl_host.clear();
     }
     return n;
 #else
-    (void)max; (void)start_end; (void)names; (void)streams; (void)reset;
+    (void)max; (void)rec4; (void)names; (void)streams; (void)reset;
     return RT_E_UNSUPPORTED;
 #endif
 }

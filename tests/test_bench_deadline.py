@@ -30,9 +30,9 @@ DRIVER = textwrap.dedent('''
     scene = rtamd.build_scene(spec)
     tot = dict(segments=73728, n_ret=1, n_slot=1, n_loc=1, n_sph=1, n_box=1, n_tri=1, n_hit=1, primary=65536,
                n_warn=0, n_fault=0, n_cull=1, n_exact=1)
-    res = dict(tot=tot, elapsed=0.01, elapsed_serial=0.02, warmup_frames=16, kernel_ms=0.1, same=True, host=None,
+    res = dict(tot=tot, elapsed=0.01, elapsed_serial=0.02, elapsed_moving=0.011, warmup_frames=16, kernel_ms=0.1, same=True, host=None,
                exposure=None, P=16, mode="one GPU", collective=None, n_gpus=1)
-    args = types.SimpleNamespace(steps=32, config="config1", stripe=8, cpu_budget=2.0, no_profile=False,
+    args = types.SimpleNamespace(steps=32, warmup=3, config="config1", stripe=8, cpu_budget=2.0, no_profile=False,
                                  profile_out=None, no_js=False, deadline=deadline_s)
     deadline = bench.Deadline(deadline_s, t0=time.monotonic())
     rep = bench.Reporter()

@@ -1,0 +1,56 @@
+"""bench.py's per-kernel roofline arithmetic on canned counter values (CPU): the clock derived from
+GRBM_GUI_ACTIVE is clamped to the 2.4 GHz peak and flagged when a short kernel's counter implies more,
+the pooled pass bytes are labelled as pooled, and SURVEY §8(d)'s HBM frame is reported as not
+applicable with its ratios to peak."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+TOT = dict(segments=2_200_000, n_ret=150_000_000, n_slot=160_000_000, n_loc=3_000_000, n_sph=10, n_box=20,
+           n_tri=1_700_000_000, n_hit=2_100_000, primary=2_073_600, n_warn=0, n_fault=0, n_cull=60_000_000,
+           n_exact=2_400_000)
+
+
+def _pmc(ms, ghz, valu=1e9, f64=1e8):
+    s = ms * 1e-3
+    return dict(SQ_INSTS_VALU=valu, SQ_INSTS_VALU_ADD_F64=f64 / 2, SQ_INSTS_VALU_MUL_F64=f64 / 2,
+                SQ_INSTS_SALU=3e8, SQ_INSTS_BRANCH=1e8, GRBM_GUI_ACTIVE=ghz * 1e9 * 8 * s,
+                SQ_THREAD_CYCLES_VALU=44.0 * valu, SQ_ACTIVE_INST_VALU=valu, SQ_WAVE_CYCLES=1e9, SQ_WAIT_ANY=5e8,
+                FETCH_SIZE=250_000.0, WRITE_SIZE=10_000.0)
+
+
+def test_clock_above_peak_is_clamped_and_flagged():
+    dur = {"k_walk_first": 2.15, "k_cont": 0.005}
+    pmc = {"k_walk_first": _pmc(2.15, 2.3), "k_cont": _pmc(0.005, 5.86, valu=1e6, f64=1e5)}
+    kr = bench.kernel_rooflines(dur, pmc, TOT)
+    w, c = kr["k_walk_first"], kr["k_cont"]
+    assert w["clock_valid"] and w["clock_ghz"] == pytest.approx(2.3, abs=1e-3)
+    assert not c["clock_valid"] and c["clock_ghz"] == bench.CLOCK_GHZ and c["clock_ghz_counter"] > 5.8
+    # the issue fraction of the short kernel is taken at the peak clock, never above what 2.4 GHz allows
+    assert c["valu_issue_frac"] == pytest.approx(c["valu_issue_frac_peak_clock"], rel=1e-3)
+    cyc = bench.ISSUE_CYC * (1e9 - 1e8) + bench.ISSUE_CYC_F64 * 1e8
+    assert w["valu_issue_frac"] == pytest.approx(cyc / (bench.SIMDS * 2.3e9 * 2.15e-3), rel=1e-3)
+
+
+def test_pooled_pass_bytes_are_labelled():
+    dur = {"k_walk_first": 2.0, "k_seg": 0.25, "k_shade": 0.1}
+    kr = bench.kernel_rooflines(dur, {k: _pmc(v, 2.3) for k, v in dur.items()}, TOT)
+    for k in ("k_walk_first", "k_seg"):
+        assert "alg_GBps" not in kr[k] and "alg_GBps_pooled" in kr[k] and "alg_frac_of_hbm_peak_pooled" in kr[k]
+    # one pool split by time share: equal rates by construction (what "pooled" says)
+    assert kr["k_walk_first"]["alg_GBps_pooled"] == pytest.approx(kr["k_seg"]["alg_GBps_pooled"], rel=1e-2)
+
+
+def test_hbm_frame_of_survey_8d_is_not_applicable():
+    h = bench.hbm_8d(TOT, 2.2197e-3, 502e6)
+    assert h["applicable"] is False
+    ref = bench.algorithmic_bytes(TOT, bench.BYTES_REF)
+    assert h["reference_equivalent_TBps"] == pytest.approx(ref / 2.2197e-3 / 1e12, rel=1e-2)
+    assert h["reference_equivalent_frac_of_peak"] > 1            # above HBM peak: not a bandwidth roof
+    assert h["hbm_counted_frac_of_peak"] == pytest.approx(502e6 / 2.2197e-3 / 8e12, rel=1e-2)

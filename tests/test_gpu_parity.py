@@ -500,6 +500,42 @@ def test_level0_segments_equal_tiles(ctx, name, k, cap, monkeypatch):
         _compare(ref, frames[0])
 
 
+SOLO_CASES = [(n, cap, seg) for n in ("config1", "small3", "small8", "transmission", "config2")
+              for cap, seg in ((None, None), ("2", None), (None, "0"), ("2", "0"))]
+
+
+@pytest.mark.parametrize("name,cap,seg", SOLO_CASES)
+def test_level_solo_equals_separate_passes(ctx, name, cap, seg, monkeypatch):
+    """A bounce level as one k_level launch: forced on every level (RT_LEVEL_SOLO=2), so
+    that its on-device fallback runs — a level that is not segmented (RT_SEG=0: one segment per ray,
+    walked, scanned and shaded by its lane), lists that overflow to k_cont (RT_CAND_CAP=2) — frames
+    identical to the separate passes (RT_LEVEL_SOLO=0) and to the oracle at refmax 5; and the
+    production default on second frames (solo levels from the hints)."""
+    spec = {"config1": scenes.config1_spheres, "small3": lambda: scenes.small_random(3),
+            "small8": lambda: scenes.small_random(8, n_tri=800, half=0.04),
+            "transmission": _transmission_spec, "config2": scenes.config2}[name]()
+    W, H = (320, 200) if name != "transmission" else (128, 128)
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(5)
+    scene = rtamd.build_scene(spec)
+    if cap:
+        monkeypatch.setenv("RT_CAND_CAP", cap)
+    if seg:
+        monkeypatch.setenv("RT_SEG", seg)
+    frames = []
+    for solo in ("2", "0", "1"):
+        monkeypatch.setenv("RT_LEVEL_SOLO", solo)
+        c = rtamd.Context(0)
+        try:
+            c.upload(scene)
+            frames.append([c.trace_frame(cam, cfg, stats=False, allow_fault=True) for _ in range(3)])
+        finally:
+            c.close()
+    for f in frames[0] + frames[2]:
+        _same_frames(f, frames[1][0])
+    w, root = oracle.build_scene(spec)
+    _compare(w.trace_frame(root, cam, cfg, nthreads=8), frames[0][0])
+
+
 def test_roughness_rejected(ctx):
     spec = scenes.config1_spheres()
     sh = spec.shades.copy()

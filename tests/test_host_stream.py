@@ -1,0 +1,123 @@
+"""Host-buffer frames streamed after level 0 (rt_api.hip trace_frame_stream).
+
+rt_trace_frame on one GPU sends the frame buffer to the host as soon as level 0 is shaded, while the
+bounce levels run, and then patches the pixels those levels and k_cont wrote (a compact list).  The
+previous ExposureBuffer values go to the device first, so a throwing frame still leaves the
+reference's partial frame.  Scheduling only: every frame equals the one-launch frame (streaming off,
+one band) and the oracle bit for bit — blends, ids, the counter RNG, glass, a late list that
+overflows (RT_LATE_CAP) and throws (src/raytracer.ts:318-329).
+"""
+import numpy as np
+import pytest
+
+import oracle
+import rtamd
+from rtamd import abi, scenes
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("rgb", "hit_entity", "hit_node", "status")
+
+
+def _same(a, b, ids=True):
+    for k in KEYS if ids else ("rgb",):
+        assert np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), k
+    assert a["rc"] == b["rc"]
+
+
+def _ctx(scene, monkeypatch, stream, cap=None):
+    monkeypatch.setenv("RT_HOST_STREAM", "1" if stream else "0")
+    monkeypatch.setenv("RT_STREAM_MIN", "0")
+    monkeypatch.setenv("RT_BANDS", "1")
+    if cap:
+        monkeypatch.setenv("RT_LATE_CAP", str(cap))
+    else:
+        monkeypatch.delenv("RT_LATE_CAP", raising=False)
+    c = rtamd.Context(0)
+    c.upload(scene)
+    return c
+
+
+@pytest.fixture(scope="module")
+def small3():
+    spec = scenes.small_random(3)
+    return spec, rtamd.build_scene(spec)
+
+
+@pytest.mark.parametrize("cap", [None, 5])
+@pytest.mark.parametrize("wh", [(160, 120), (101, 37), (33, 200)])
+def test_streamed_equals_one_launch(small3, wh, cap, monkeypatch):
+    """Ids on and off, a second and third frame (late-list capacity from the grid hints), and a blend;
+    cap 5: the late list overflows and the frame is copied again whole."""
+    spec, scene = small3
+    cam, cfg = scenes.make_camera(*wh), scenes.make_config(3)
+    one = _ctx(scene, monkeypatch, False)
+    st = _ctx(scene, monkeypatch, True, cap)
+    try:
+        ref = one.trace_frame(cam, cfg, stats=False, allow_fault=True)
+        for _ in range(3):
+            _same(ref, st.trace_frame(cam, cfg, stats=False, allow_fault=True))
+        got = st.trace_frame(cam, cfg, ids=False, stats=False, allow_fault=True)
+        assert np.array_equal(ref["rgb"].view(np.uint32), got["rgb"].view(np.uint32))
+        bcfg = scenes.make_config(3, col_weight=1 / 3)
+        old = np.random.default_rng(7).uniform(0, 2, wh[0] * wh[1] * 3).astype(np.float32)
+        _same(one.trace_frame(cam, bcfg, rgb=old.copy(), stats=False, allow_fault=True),
+              st.trace_frame(cam, bcfg, rgb=old.copy(), stats=False, allow_fault=True))
+    finally:
+        one.close()
+        st.close()
+
+
+def test_streamed_equals_oracle_scatter_and_transmission(monkeypatch):
+    """Rough mirrors on the counter RNG and glass at refmax 5 (many late pixels), against the oracle."""
+    spec = scenes.roughen(scenes.small_random(4, p_mirror=0.5))
+    cam = scenes.make_camera(200, 150)
+    cfg = scenes.make_config(5, scatter_seed=123456789012345)
+    c = _ctx(rtamd.build_scene(spec), monkeypatch, True)
+    try:
+        got = [c.trace_frame(cam, cfg, stats=False, allow_fault=True) for _ in range(2)][-1]
+    finally:
+        c.close()
+    w, root = oracle.build_scene(spec)
+    ref = w.trace_frame(root, cam, cfg, nthreads=8)
+    assert np.array_equal(ref["rgb"].view(np.uint32), got["rgb"].view(np.uint32))
+    for k in ("hit_entity", "hit_node", "status"):
+        assert np.array_equal(ref[k], got[k]), k
+
+
+def _throwing_scene():
+    """Glass spheres seen from an undefined substance: refract_ray throws (test_bands' scene)."""
+    spec = scenes.config1_spheres()
+    e, sh = spec.entities.copy(), spec.shades.copy()
+    sh["response"][:] = abi.RT_RESP_TRANSMISSION
+    sh["light"][:] = 0
+    e["substance"][:] = 2
+    e["substance"][-1] = -1
+    return scenes.SceneSpec("throws", e, sh)
+
+
+@pytest.mark.parametrize("blend", [0.5, 1.0])
+@pytest.mark.parametrize("ids", [True, False])
+def test_streamed_keeps_the_reference_partial_frame(blend, ids, monkeypatch):
+    """A throwing frame: pixels before the first throw in scan order final, it and every later one
+    the previous value (restored from the device copy of the previous values), bit for bit with the
+    oracle's aborted frame."""
+    spec = _throwing_scene()
+    W, H = 96, 72
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(5, default_substance=-1, col_weight=blend)
+    old = np.random.default_rng(5).random(W * H * 3, dtype=np.float32)
+    w, root = oracle.build_scene(spec)
+    try:
+        want = w.trace_frame(root, cam, cfg, rgb=old.copy(), abort=True)
+    finally:
+        w.close()
+    c = _ctx(rtamd.build_scene(spec), monkeypatch, True)
+    try:
+        got = c.trace_frame(cam, cfg, rgb=old.copy(), ids=ids, stats=False, allow_fault=True)
+    finally:
+        c.close()
+    assert got["rc"] == abi.RT_E_FAULT
+    assert np.array_equal(got["rgb"].view(np.uint32), want["rgb"].view(np.uint32))
+    assert not np.array_equal(got["rgb"].view(np.uint32), old.view(np.uint32))
+    if ids:
+        assert np.array_equal(got["status"], want["status"])

@@ -88,23 +88,50 @@ def test_rccl_gather_one_rank(small3, single, monkeypatch):
         m.close()
 
 
+@pytest.mark.parametrize("stats", [True, False])
 @pytest.mark.parametrize("devices", [[0, 0, 0], [0, 0, 0, 0, 0, 0, 0]])
-def test_blend_over_parts(small3, single, devices):
+def test_blend_over_parts(small3, single, devices, stats):
     """ExposureBuffer blend (col_weight != 1) on a split frame: the current frame is dealt out to
-    the parts first, each part blends in binary64 as the one-device frame does."""
+    the parts first (the gather path: k_stripes + scatter; without counters: each part's stripes
+    copied from the host buffer to its device), each part blends in binary64 as the one-device frame
+    does."""
     spec, scene = small3
-    cam, cfg = scenes.make_camera(64, 48), scenes.make_config(2, col_weight=1 / 3)
-    old = np.random.default_rng(0).uniform(0, 2, 64 * 48 * 3).astype(np.float32)
+    cam, cfg = scenes.make_camera(64, 45), scenes.make_config(2, col_weight=1 / 3)
+    old = np.random.default_rng(0).uniform(0, 2, 64 * 45 * 3).astype(np.float32)
     m = _ctx(scene, devices=devices)
     try:
         _same(single.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True),
-              m.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True))
+              m.trace_frame(cam, cfg, rgb=old.copy(), stats=stats, allow_fault=True))
     finally:
         m.close()
     w, root = oracle.build_scene(spec)
     ref = w.trace_frame(root, cam, cfg, rgb=old.copy())
     got = single.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True)
     assert np.array_equal(ref["rgb"].view(np.uint32), got["rgb"].view(np.uint32))
+
+
+@pytest.mark.parametrize("direct", ["1", "0"])
+@pytest.mark.parametrize("ids", [True, False])
+@pytest.mark.parametrize("devices,stripe,wh", [([0, 0], 8, (160, 120)), ([0] * 8, 8, (200, 135)),
+                                               ([0] * 3, 5, (101, 37)), ([0] * 5, 500, (64, 48))])
+def test_host_frame_parts_copied_per_device(small3, single, devices, stripe, wh, ids, direct, monkeypatch):
+    """The multi-device host frame without counters: each device copies its own stripes into the host
+    buffer (2D copies; a partial last stripe; empty parts), ids on and off; RT_HOST_DIRECT=0 is the
+    gather to devices[0] and one D2H.  Both equal the one-device frame bit for bit."""
+    monkeypatch.setenv("RT_HOST_DIRECT", direct)
+    spec, scene = small3
+    cam, cfg = scenes.make_camera(*wh), scenes.make_config(3)
+    ref = single.trace_frame(cam, cfg, stats=False, allow_fault=True)
+    m = _ctx(scene, devices=devices, stripe_rows=stripe)
+    try:
+        for _ in range(2):
+            got = m.trace_frame(cam, cfg, ids=ids, stats=False, allow_fault=True)
+            assert got["rc"] == ref["rc"]
+            assert np.array_equal(ref["rgb"].view(np.uint32), got["rgb"].view(np.uint32))
+            if ids:
+                _same(ref, got)
+    finally:
+        m.close()
 
 
 @pytest.mark.parametrize("gather", ["peer", "rccl"])
@@ -181,8 +208,9 @@ def test_frame_fault_reports_reference_throws():
             m.close()
 
 
+@pytest.mark.parametrize("stats", [True, False])
 @pytest.mark.parametrize("kw", [dict(device=0), dict(devices=[0, 0, 0], stripe_rows=3)])
-def test_throw_keeps_the_reference_partial_frame(kw):
+def test_throw_keeps_the_reference_partial_frame(kw, stats):
     """After a throw the reference's ExposureBuffer holds the pixels traced before the first throwing
     pixel in scan order; that pixel and all later ones keep their previous value
     (src/raytracer.ts:318-329).  rt_trace_frame leaves the same buffer, bit for bit with the oracle."""
@@ -198,7 +226,7 @@ def test_throw_keeps_the_reference_partial_frame(kw):
     assert (st == 2).any() and (st == 0).any()
     m = _ctx(rtamd.build_scene(spec), **kw)
     try:
-        got = m.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True)
+        got = m.trace_frame(cam, cfg, rgb=old.copy(), stats=stats, allow_fault=True)
     finally:
         m.close()
     assert got["rc"] == abi.RT_E_FAULT

@@ -30,7 +30,7 @@ from rtamd import scenes  # noqa: E402
 
 def read_timeline(lib, reset):
     n_max = 1 << 16
-    se = (C.c_ulonglong * (2 * n_max))()
+    se = (C.c_ulonglong * (4 * n_max))()
     names = C.create_string_buffer(64 * n_max)
     streams = (C.c_ulonglong * n_max)()
     lib.rt_debug_timeline.restype = C.c_int
@@ -40,7 +40,7 @@ def read_timeline(lib, reset):
     out = []
     for i in range(n):
         nm = names.raw[64 * i:64 * i + 64].split(b"\0")[0].decode()
-        out.append((se[2 * i], se[2 * i + 1], nm, streams[i]))
+        out.append((se[4 * i], se[4 * i + 1], nm, streams[i], se[4 * i + 2], se[4 * i + 3]))
     return out
 
 
@@ -59,21 +59,28 @@ def analyse(recs, frames):
         prev = t
     tot = sum(hist.values()) or 1
     per = collections.defaultdict(list)
-    for s, e, n, _ in recs:
+    wave_us = collections.defaultdict(float)
+    waves = collections.defaultdict(int)
+    for s, e, n, _, wt, wn in recs:
         per[n].append((e - s) * 1e-2)                                 # 10 ns ticks -> us
+        wave_us[n] += wt * 1e-2
+        waves[n] += wn
     gaps = collections.defaultdict(list)                              # launch start - previous launch end, same stream
     last = {}
-    for s, e, n, st in sorted(recs):
+    for s, e, n, st, *_ in sorted(recs):
         if st in last:
             gaps[n].append((s - last[st]) * 1e-2)
         last[st] = e
     return dict(
         wall_us_per_frame=round((t1 - t0) * 1e-2 / frames, 1),
+        wave_ms_per_frame=round(sum(r[4] for r in recs) * 1e-5 / frames, 3),
         busy_frac=round(1 - hist.get(0, 0) / tot, 3),
         mean_concurrency=round(sum(k * v for k, v in hist.items()) / tot, 2),
         concurrency={k: round(v / tot, 3) for k, v in sorted(hist.items())},
         kernels={n: dict(calls=len(v), mean_us=round(float(np.mean(v)), 1), per_frame_us=round(sum(v) / frames, 1),
                          max_us=round(float(np.max(v)), 1),
+                         waves_per_frame=round(waves[n] / frames, 1),
+                         wave_ms_per_frame=round(wave_us[n] / frames / 1e3, 3),
                          gap_us=round(float(np.median(gaps[n])), 1) if gaps[n] else None)
                  for n, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))})
 
