@@ -145,15 +145,10 @@ struct rt_ctx {
     // entries: config 3 (101 k entries) 4 % faster; config 5 (1 M) runs its long
     // candidate scans faster in k_first's own launch (6 waves/SIMD against 4), 17.9 against 18.2 ms.
     int64_t wf_list = 1 << 19;
-    // Level 0 with K segments per primary ray: RT_L0_SEG = K (2 / 4 / 8), or 0 for
-    // automatic (the least K with at least l0_fill work items per resident wave of k_walk_first).
-    // Default 1, off: measured slower at every part size (a wave's two walk phases cost their union)
-    int l0_seg = 1;
     int l0_bs = 64;                  // RT_L0_BS: threads per block of the level-0 walk + first-hit kernel
     bool shade_hint = true;          // RT_SHADE_HINT=0: level 0's k_shade on the full persistent grid
     int level_solo = 1;              // RT_LEVEL_SOLO=0: every level's five kernels, predicted no-ops on 8 blocks
                                      // (2, tests: every bounce level as k_level)
-    int l0_fill = 4;
     int64_t band_min = 1 << 20;      // RT_BAND_MIN: frames of fewer pixels run as one launch (256^2: 0.44 ms
                                      // one launch against 0.61 in 2 bands; 1080p and up gain, §5.14)
     // Host-buffer frames on one GPU streamed after level 0 (trace_frame_stream): the
@@ -260,8 +255,6 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_FUSE_MAX")) c->fuse_max = atoll(e) < 0 ? 0 : atoll(e);
     if (const char *e = getenv("RT_FUSE_LIST")) c->fuse_list = atoll(e) < 0 ? 0 : atoll(e);
     if (const char *e = getenv("RT_WF_LIST")) c->wf_list = atoll(e);
-    if (const char *e = getenv("RT_L0_SEG")) c->l0_seg = atoi(e) <= 0 ? -1 : (atoi(e) == 1 ? 1 : pow2_at_most_64(std::min(atoi(e), 8)));
-    if (const char *e = getenv("RT_L0_FILL")) c->l0_fill = std::max(0, atoi(e));
     if (const char *e = getenv("RT_L0_BS")) c->l0_bs = atoi(e) == 64 ? 64 : 256;
     if (const char *e = getenv("RT_SHADE_HINT")) c->shade_hint = atoi(e) != 0;
     if (const char *e = getenv("RT_LEVEL_SOLO")) c->level_solo = std::min(2, std::max(0, atoi(e)));
@@ -625,23 +618,14 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.l0_bs = c->l0_bs;
     L.shade_hint = c->shade_hint && c->hints;
     L.level_solo = c->level_solo == 2 ? 2 : (c->level_solo && c->hints);
+
     L.blend = cfg->col_weight != 1.0;
     if (c->split && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).
-        // level 0 in K segments per primary ray when the part has few tiles per resident wave of
-        // k_walk_first (4 waves per SIMD, 16 per CU): the lists then hold K * P rays
-        int K = 1;
-        if (L.walk_first && c->l0_seg != 1) {
-            const long long tiles = (long long)((cam->width + 7) / 8) * ((rows + 7) / 8), waves = 16ll * d.n_cu;
-            if (c->l0_seg > 1) K = c->l0_seg;
-            else
-                while (K < 8 && tiles * K < (long long)c->l0_fill * waves) K *= 2;
-        }
-        L.l0_seg = K > 1 ? K : 0;
-        // the walk kernels address the lists with 32-bit byte offsets (cand_store): cand_cap * K * P * 4 < 2^32
-        L.cand_cap = (int32_t)std::min<long long>(c->cand_cap, ((1ll << 32) - 1) / (4ll * K * P));
-        if (d.b_cand.ensure(sizeof(int32_t) * (size_t)L.cand_cap * (size_t)K * P) == RT_OK &&
+        // the walk kernels address the lists with 32-bit byte offsets (cand_store): cand_cap * P * 4 < 2^32
+        L.cand_cap = (int32_t)std::min<long long>(c->cand_cap, ((1ll << 32) - 1) / (4ll * P));
+        if (d.b_cand.ensure(sizeof(int32_t) * (size_t)L.cand_cap * P) == RT_OK &&
             d.b_cand_n.ensure(2 * sizeof(int32_t) * P) == RT_OK && d.b_first.ensure(2 * sizeof(int32_t) * P) == RT_OK &&
             d.b_queue.ensure(3 * sizeof(RtCont) * P) == RT_OK) {
             L.cand = (int32_t *)d.b_cand.p;
@@ -656,7 +640,6 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
             L.cand = nullptr;
             L.cand_n = nullptr;
             L.first = nullptr;
-            L.l0_seg = 0;
         }
     }
     return RT_OK;

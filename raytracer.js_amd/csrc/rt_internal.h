@@ -120,12 +120,7 @@ struct RtFrameSetup {
     int32_t start_oct;
     int32_t start_sub;    // start substance (-1: undefined)
     int32_t fault;
-    // the camera seat's tree and its ancestors up to the root (the nodes the reference's walk returns
-    // on its way out of them); n_chain = -1 when longer than RT_CHAIN (k_walk_first_seg keeps all)
-    int32_t n_chain;
-    int32_t chain[31];
 };
-enum { RT_CHAIN = 31 };
 
 // Counter slots (rt_stats order).
 enum { CT_SEG, CT_RET, CT_SLOT, CT_LOC, CT_SPH, CT_BOX, CT_TRI, CT_HIT, CT_PRIM, CT_WARN, CT_FAULT,
@@ -222,7 +217,6 @@ struct RtLaunch {
     int32_t refill_always;                      // refill every wide level, not only where a recent frame had one (tests)
     int32_t seg_max;                            // bounce levels of more rays run unsegmented (0: no limit; RT_SEG_MAX)
     int32_t walk_first;                         // level 0 as one walk + first-hit kernel (k_walk_first; §5.18)
-    int32_t l0_seg;                             // > 1: level 0 with K segments per primary ray (k_walk_first_seg; §5.20)
     int32_t tl;                                 // RT_TL builds: this launch's timeline record (-1: none)
     int32_t l0_bs;                              // threads per block of k_walk_first (RT_L0_BS: 64 or 256)
     int32_t shade_hint;                         // level 0's k_shade grid from a recent frame's queue (RT_SHADE_HINT)

@@ -1203,15 +1203,12 @@ __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_des
             cur = reinterpret_cast<const int2 *>(S.node_up)[cur].x;
         }
         if (lane == 0) {
-            setup->fault = r < 0;
-            setup->start_tree = r == 1 ? t : -1;
-            setup->start_oct = oc;
-            setup->start_sub = se >= 0 ? S.ent_sub[se] : cfg.default_substance;
-            int n = 0;
-            for (int a = r == 1 ? t : -1; a >= 0 && n <= RT_CHAIN; a = reinterpret_cast<const int2 *>(S.node_up)[a].x)
-                if (n < RT_CHAIN) setup->chain[n++] = a;
-                else n = RT_CHAIN + 1;
-            setup->n_chain = n > RT_CHAIN ? -1 : n;
+            RtFrameSetup f;
+            f.fault = r < 0;
+            f.start_tree = r == 1 ? t : -1;
+            f.start_oct = oc;
+            f.start_sub = se >= 0 ? S.ent_sub[se] : cfg.default_substance;
+            *setup = f;
         }
         return;
     }
@@ -2355,134 +2352,6 @@ __global__ void __launch_bounds__(BS, MINW) k_walk_first(RtLaunch L)
     }
 }
 
-// Level 0 of a small part with segmented primary rays (L.l0_seg = K > 1).  A part
-// of an 8-GPU frame has about one 8x8 tile per resident wave, so k_walk_first's time is its slowest
-// tile.  Here each primary ray is cut into K segments along its root-cube crossing exactly as the
-// bounce levels' rays are (§5.10: segment 0 is the reference walk from the camera's seat, segment
-// j >= 1 is seated in the slot holding the point at j/K of the crossing, and each stops on reaching
-// the next valid segment's seat), and a wave takes 64 / K rays of an 8 x (8 / K) pixel tile with K
-// adjacent lanes per ray: K times more work items, each about 1/K of a tile's walk.  The wave then
-// scans its segments' lists (seg_first_item's rule: a segment is scanned only if every earlier one
-// reached its successor), and the lane of each ray's segment 0 finishes the ray as first_item does
-// (early_shade, or the level-0 shading queue), with the combined end status in cand_n[pixel] for
-// k_shade.  Lists: ray pixel * K + segment, stride K * pixels (prepare sizes the buffer).
-template <int MINW>
-__global__ void __launch_bounds__(256, MINW) k_walk_first_seg(RtLaunch L)
-{
-    TL_SCOPE(L.tl);
-    const int lane = threadIdx.x & 63;
-    const RtFrameSetup F = *L.setup;
-    const RtDevScene &S = L.scene;
-    const int K = L.l0_seg, th = 8 / K;                      // K in {2, 4, 8}: tiles of 8 x th pixels
-    const int W = L.cam.width;
-    const int tiles_x = (W + 7) >> 3;
-    const int items = tiles_x * ((L.rows + th - 1) / th);
-    const size_t P = (size_t)L.rows * (size_t)W;
-    const uint32_t stride = (uint32_t)(P * (size_t)K);
-    const int j = lane & (K - 1), base = lane & ~(K - 1), r = lane / K;
-    const double frac = (double)j / (double)K;
-    const bool fault = F.fault != 0;
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    stage_top(S);
-    for (;;) {
-        int t_end;
-        const int t = claim_xcd(pass_heads(L, 0, 1), items, lane, 1, t_end, L.xcd_mask & 1);
-        if (t >= items) break;
-        const int ty = t / tiles_x, tx = t - ty * tiles_x;
-        const int x = tx * 8 + (r & 7), lr = ty * th + (r >> 3);
-        const bool valid = x < W && lr < L.rows;
-        RaySrc src;
-        src.valid = valid;
-        src.rec = nullptr;
-        src.id = valid ? (size_t)lr * (size_t)W + (size_t)x : 0;
-        src.pix = (int)src.id;
-        for (int i = 0; i < 3; i++) {
-            src.o[i] = L.cam.pos[i];
-            src.d[i] = valid ? L.dirs[(size_t)i * P + (size_t)x * (size_t)L.rows + (size_t)lr] : 1.0;   // x-major
-        }
-        const uint32_t id = (uint32_t)(src.id * (size_t)K + (size_t)j);
-        // this lane's segment: its seat, or none (SEG_SKIP)
-        Walker w;
-        int end = SEG_SKIP, seat = -1;
-        if (valid) {
-            if (j == 0) {
-                end = !fault && walker_set(S, w, src.o, src.d, F.start_tree >= 0, F.start_tree, F.start_oct, c) >= 0
-                          ? SEG_FIN : SEG_THROW;
-            } else if (!fault && F.start_tree >= 0) {
-                const NodeDims rt = node_dims(S, 0);
-                BoxIsect bi;
-                if (box_isect(rt.x + 0.5 * rt.s, rt.y + 0.5 * rt.s, rt.z + 0.5 * rt.s, rt.s, src.o, src.d, bi)) {
-                    const double t0 = bi.u1 > 0 ? bi.u1 : 0.0, t1 = bi.u2;
-                    if (t1 > t0 && t1 < 1e300) {
-                        const double tt = t0 + (t1 - t0) * frac;
-                        const double p[3] = {src.o[0] + src.d[0] * tt, src.o[1] + src.d[1] * tt, src.o[2] + src.d[2] * tt};
-                        int tree = -1, oct = 0;
-                        if (node_at_pos(S, p, tree, oct, c.loc) == 1 &&
-                            walker_set(S, w, src.o, src.d, true, tree, oct, c) >= 0) {
-                            seat = tree * 8 + oct;
-                            end = SEG_FIN;
-                        }
-                    }
-                }
-            }
-        }
-        int stop = -1;                                   // the seat of the next segment that has one
-        for (int k = 1; k < K; k++) {
-            const int s = __shfl(seat, base | (j + k < K ? j + k : K - 1), 64);
-            if (stop < 0 && j + k < K && s >= 0) stop = s;
-        }
-        int n = 0;
-        if (end == SEG_FIN) {
-            const RayBox rb = make_raybox(w.o, w.d);
-            // A segment j >= 1 returns the ancestors of its seat when it climbs out of them (a step_back
-            // at depth 0: F_STEPPED is set when the next head returns the slot's node).  An ancestor
-            // that does not hold the camera's seat was entered, and returned, by the reference walk
-            // before it reached this seat: its entities were tested and missed, so the list drops it.
-            // The camera seat's own ancestors are returned on the way out by the reference too: kept.
-            const int n_chain = F.n_chain;
-            auto emit = [&](int node) {
-                if (j > 0 && (w.flags & F_STEPPED) && n_chain >= 0) {
-                    bool cam = false;
-                    for (int a = 0; a < n_chain; a++) cam = cam || L.setup->chain[a] == node;
-                    if (!cam) return;
-                }
-                if (!node_candidate(S, node, L.cull != 0, rb)) return;
-                if (n < L.cand_cap) cand_store(L, n, stride, id, node);
-                n++;
-            };
-            const int rr = walker_run<true>(S, w, emit, stop);
-            if (rr < 0) end = rr == -2 ? SEG_CAP : SEG_THROW;
-            else if (rr == 2) end = SEG_REACHED;
-        }
-        const int cn = valid ? (n > L.cand_cap ? -1 : n * 8 + end) : SEG_SKIP;
-        // the scan of this lane's list if every earlier segment of the ray reached its successor
-        bool open = true;
-        for (int k = 0; k < K - 1; k++) {
-            const int s = __shfl(cn, base | k, 64);
-            if (k < j && !(s >= 0 && ((s & 7) == SEG_REACHED || (s & 7) == SEG_SKIP))) open = false;
-        }
-        int2 res = make_int2(-1, -1);
-        if (valid && open && cn >= 8 && !fault)
-            res = scan_first<false>(L, S, src.o, src.d, make_raybox(src.o, src.d), stride, id, cn >> 3, c);
-        // in segment order: an overflow sends the ray to k_cont; a hit wins; an end ends the ray
-        bool done = false;
-        int2 out = make_int2(-1, -1);
-        int ocn = 0;
-        for (int k = 0; k < K; k++) {
-            const int s = __shfl(cn, base | k, 64);
-            const int rx = __shfl(res.x, base | k, 64), ry = __shfl(res.y, base | k, 64);
-            if (done) continue;
-            if (s < 0) { done = true; ocn = -1; }
-            else if (ry >= 0) { done = true; out = make_int2(rx, ry); ocn = 4; }
-            else if ((s & 7) != SEG_REACHED && (s & 7) != SEG_SKIP) { done = true; ocn = s & 3; }
-        }
-        if (valid && j == 0) {
-            L.cand_n[src.id] = ocn;                      // k_shade's level-0 status (-1 overflow, end & 3)
-            first_finish(L, src, ocn, out, fault);
-        }
-    }
-}
-
 // The shading of one resolved segment (k_shade, k_seg): the pixel is written when the ray ends, a
 // continuation is queued for the next level, an overflowed list (cn < 0) goes to k_cont.  `fh` =
 // first[ray] (k_first's {node, slot}).
@@ -2784,8 +2653,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             RtLaunch Lw = Lv;                         // the walk kernels read the upper levels from LDS
             Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
             const size_t lds = sizeof(RtNode) * (size_t)Lw.scene.n_lds;
-            if (L.l0_seg > 1 && lv == 0) launch_persistent(k_walk_first_seg<4>, st, Lw, mb, lds);
-            else if (L.walk_first && lv == 0) {
+            if (L.walk_first && lv == 0) {
                 // one wave per block: a part of an 8-GPU frame gives each wave about one tile, and a
                 // 4-wave block would hold its SIMD slots until its slowest tile ends
                 if (L.l0_bs == 64) launch_persistent(k_walk_first<4, 64>, st, Lw, mb, lds, 64);
@@ -2862,7 +2730,7 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *na
             {(const void *)k_trace<false, 2>, "k_trace"}, {(const void *)k_trace<false, 3>, "k_trace"},
             {(const void *)k_trace<false, 4>, "k_trace"}, {(const void *)k_walk_first<4>, "k_walk_first"},
             {(const void *)k_walk_first<4, 64>, "k_walk_first"},
-            {(const void *)k_walk_first_seg<4>, "k_walk_first_seg"}, {(const void *)k_walk<3>, "k_walk"},
+{(const void *)k_walk<3>, "k_walk"},
             {(const void *)k_walk<4>, "k_walk"}, {(const void *)k_walk<5>, "k_walk"},
             {(const void *)k_seg<2, false>, "k_seg_wide"}, {(const void *)k_seg<2, true>, "k_seg"},
             {(const void *)k_level<2>, "k_level"},

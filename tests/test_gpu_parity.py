@@ -457,49 +457,6 @@ def test_segmented_equals_unsegmented(ctx, name, cap, k, thin, monkeypatch):
     _compare(w.trace_frame(root, cam, cfg, nthreads=8), a)
 
 
-L0_SEG_CASES = [(n, k, cap) for n in ("config1", "small3", "small8", "transmission", "config2") for k in (2, 4, 8)
-                for cap in (None, "2")] + [("reseat", 4, None)]
-
-
-@pytest.mark.parametrize("name,k,cap", L0_SEG_CASES)
-def test_level0_segments_equal_tiles(ctx, name, k, cap, monkeypatch):
-    """Level 0 with k segments per primary ray (k lanes per camera ray, each walking
-    one stretch of its root crossing; the production choice for parts with few tiles per resident
-    wave) changes scheduling, not results: frames identical to whole-ray tiles (RT_L0_SEG=1) and to
-    the oracle at refmax 5, also when segment lists overflow (RT_CAND_CAP=2) and on a scene whose
-    walks throw (the post-light re-seat scene)."""
-    spec = {"config1": scenes.config1_spheres, "small3": lambda: scenes.small_random(3),
-            "small8": lambda: scenes.small_random(8, n_tri=800, half=0.04),
-            "transmission": _transmission_spec, "config2": scenes.config2,
-            "reseat": lambda: scenes.reseat_throw_scene(False)[0]}[name]()
-    W, H = (320, 200) if name != "transmission" else (128, 128)
-    cam, cfg = scenes.make_camera(W, H), scenes.make_config(5)
-    if name == "reseat":
-        cam = scenes.reseat_throw_scene(False)[1]
-    scene = rtamd.build_scene(spec)
-    if cap:
-        monkeypatch.setenv("RT_CAND_CAP", cap)
-    frames = []
-    for kk in (str(k), "1"):
-        monkeypatch.setenv("RT_L0_SEG", kk)
-        c = rtamd.Context(0)
-        try:
-            c.upload(scene)
-            frames.append(c.trace_frame(cam, cfg, stats=False, allow_fault=True))
-        finally:
-            c.close()
-    _same_frames(frames[0], frames[1])
-    assert frames[0]["rc"] == frames[1]["rc"]
-    w, root = oracle.build_scene(spec)
-    ref = w.trace_frame(root, cam, cfg, nthreads=8)
-    if name == "reseat":                 # a faulting frame: the colours are the reference's partial frame
-        assert frames[0]["rc"] == abi.RT_E_FAULT
-        for key in ("hit_entity", "hit_node", "status"):
-            assert np.array_equal(ref[key], frames[0][key]), key
-    else:
-        _compare(ref, frames[0])
-
-
 SOLO_CASES = [(n, cap, seg) for n in ("config1", "small3", "small8", "transmission", "config2")
               for cap, seg in ((None, None), ("2", None), (None, "0"), ("2", "0"))]
 

@@ -238,13 +238,11 @@ def test_throw_keeps_the_reference_partial_frame(kw, stats):
     assert np.array_equal(got["rgb"].reshape(-1, 3)[kept], old.reshape(-1, 3)[kept])
 
 
-@pytest.mark.parametrize("parts,l0_seg", [(4, None), (8, None), (8, "2"), (8, "1")])
-def test_config3_split_over_parts(parts, l0_seg, monkeypatch):
+@pytest.mark.parametrize("parts", [4, 8])
+def test_config3_split_over_parts(parts):
     """BASELINE config 3 at 1920x1080 as 4 and 8 parts (the driver's N = 8 workload, one GPU's share
     each): bit-identical to the one-part frame, which test_baseline_config_full_frame holds to the
-    oracle.  Such parts run level 0 with segmented primary rays (auto, or forced K)."""
-    if l0_seg:
-        monkeypatch.setenv("RT_L0_SEG", l0_seg)
+    oracle."""
     factory, W, H, refmax = scenes.WORKLOADS["config3"]
     scene = rtamd.build_scene(factory())
     cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
