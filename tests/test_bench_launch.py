@@ -55,7 +55,7 @@ def test_kernel_names_and_rooflines():
     assert w["binding_roof"] == "valu-issue"
     # the walk pass's algorithmic bytes are split between k_walk and k_walk_seg by time
     walk_bytes = 48 * 10 + 32 * 20 + 40 * 30
-    assert w["alg_bytes_cache_served"] + kr["k_walk_seg"]["alg_bytes_cache_served"] == pytest.approx(walk_bytes, abs=2)
+    assert w["alg_bytes_cache_served_pooled"] + kr["k_walk_seg"]["alg_bytes_cache_served_pooled"] == pytest.approx(walk_bytes, abs=2)
     assert list(kr) == ["k_walk", "k_first", "k_walk_seg"]          # by time
 
 
@@ -74,9 +74,9 @@ def test_fused_level0_pools_walk_and_first_bytes():
     counters = dict(n_ret=10, n_slot=20, n_loc=30, n_cull=40, n_exact=50, n_hit=60, segments=70, primary=7)
     kr = bench.kernel_rooflines(dur, {}, counters)
     pool = 48 * 10 + 32 * 20 + 40 * 30 + 32 * 40 + 80 * 50
-    got = sum(kr[k]["alg_bytes_cache_served"] for k in dur)
+    got = sum(kr[k]["alg_bytes_cache_served_pooled"] for k in dur)
     assert got == pytest.approx(pool, abs=3)
-    assert kr["k_walk_first"]["alg_bytes_cache_served"] == pytest.approx(pool * 3.0 / 4.0, abs=2)
+    assert kr["k_walk_first"]["alg_bytes_cache_served_pooled"] == pytest.approx(pool * 3.0 / 4.0, abs=2)
 
 
 def test_default_frames_in_flight():
