@@ -161,7 +161,10 @@ struct rt_ctx {
     // (trace_frame_parts_host; RT_HOST_DIRECT=0 restores the gather to devices[0] and one D2H)
     bool host_direct = true;
     hipStream_t copy = nullptr;      // dev[0]: the level-0 D2H (and the H2D of the previous values)
+    hipStream_t aux = nullptr;       // dev[0]: the second half of level 0's walk (RT_STREAM_SPLIT)
     hipEvent_t ev_l0 = nullptr;      // level 0 shaded
+    hipEvent_t ev_fs = nullptr, ev_h1 = nullptr, ev_h2 = nullptr;   // frame start; level-0 halves done
+    bool stream_split = true;        // RT_STREAM_SPLIT=0: one level-0 launch, the frame sent after level 0
     DevBuf g_old, b_late;            // dev[0]: the previous ExposureBuffer values; the late-pixel list
     int32_t *h_info = nullptr;       // pinned: fault flag, late-pixel count
     int n_band = 0;                  // band states initialised
@@ -262,6 +265,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_HOST_STREAM")) c->host_stream = atoi(e) != 0;
     if (const char *e = getenv("RT_STREAM_MIN")) c->stream_min = atoll(e) < 0 ? 0 : atoll(e);
     if (const char *e = getenv("RT_LATE_CAP")) c->late_cap = atoll(e) < 0 ? 0 : atoll(e);
+    if (const char *e = getenv("RT_STREAM_SPLIT")) c->stream_split = atoi(e) != 0;
     if (const char *e = getenv("RT_HOST_DIRECT")) c->host_direct = atoi(e) != 0;
     if (const char *e = getenv("RT_BANDS")) c->bands = atoi(e) < 1 ? 1 : (atoi(e) > RT_MAX_BANDS ? RT_MAX_BANDS : atoi(e));
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
@@ -346,7 +350,9 @@ extern "C" void rt_destroy(rt_ctx *c)
                       &c->g_old, &c->b_late})
         b->release();
     if (c->copy) (void)hipStreamSynchronize(c->copy), (void)hipStreamDestroy(c->copy);
-    if (c->ev_l0) (void)hipEventDestroy(c->ev_l0);
+    if (c->aux) (void)hipStreamSynchronize(c->aux), (void)hipStreamDestroy(c->aux);
+    for (hipEvent_t e : {c->ev_l0, c->ev_fs, c->ev_h1, c->ev_h2})
+        if (e) (void)hipEventDestroy(e);
     if (c->h_info) (void)hipHostFree(c->h_info);
     for (int b = 0; b < RT_MAX_BANDS; b++) release_device(c->band[b]);
     if (c->h_fault) (void)hipHostFree(c->h_fault);
@@ -1000,30 +1006,59 @@ static int trace_frame_bands(rt_ctx *c, const rt_camera_desc *cam, const rt_conf
 // ExposureBuffer values travel to the device first (H2D, overlapping level 0), so that a frame with a
 // reference throw still leaves the reference's partial frame (§3.3): the host restores them from there.
 // *done = false when the frame cannot stream (the fused kernel runs it): the caller takes another path.
+// *no_hint: the frame did not stream because no frame of this context has counted its rays yet (the
+// caller runs it as one launch on dev[0], whose counters the next frame reads).
 static int trace_frame_stream(rt_ctx *c, const rt_camera_desc *cam, const rt_config_desc *cfg, float *rgb_inout,
-                              int32_t *hit_entity, int32_t *hit_node, uint8_t *status, bool *done)
+                              int32_t *hit_entity, int32_t *hit_node, uint8_t *status, bool *done, bool *no_hint)
 {
     RtDevice &d0 = c->dev[0];
     const int W = cam->width, H = cam->height;
     const size_t P = (size_t)W * (size_t)H;
     const bool ids = hit_entity || hit_node, blend = cfg->col_weight != 1.0;
     *done = false;
+    *no_hint = false;
     RtLaunch L;
     int r;
+    // streamed only when a recent frame of this context left few pixels after level 0 (queued to
+    // level 1 or k_cont: config 3 ~1 %): the late list and its host patch are per pixel, and a frame
+    // whose bounce levels rewrite most pixels (config 5: millions) is faster copied once at its end
+    if (c->late_cap <= 0) {
+        const int32_t *h = d0.ctr_snap.empty() ? nullptr : d0.ctr_snap.data();
+        const long long late_hint = h && h[4] >= 0 && h[0] >= 0 ? (long long)h[4] + h[0] : -1;
+        if (late_hint < 0 || late_hint * 32 > (long long)P) {
+            *no_hint = late_hint < 0;
+            return RT_OK;
+        }
+    }
     if ((r = prepare(c, d0, cam, cfg, 0, 1, H, WANT_STATUS | (ids ? WANT_IDS : 0), L)) != RT_OK) return r;
     if (!L.cand) return RT_OK;                                          // fused: not streamable
-    // the late list: twice the pixels a recent frame left after level 0 (queued to level 1 or k_cont),
-    // at least 2^16; more than that falls back to copying the whole frame again
+    // the late list: twice the pixels a recent frame left after level 0 (with level 0 in halves, also
+    // those level 0's k_shade wrote), at least 2^16; more than that falls back to copying the whole
+    // frame again
     const int32_t *h = L.ctr_hint;
-    const long long late_hint = h && h[4] >= 0 && h[0] >= 0 ? (long long)h[4] + h[0] : -1;
+    const bool halves = c->stream_split && L.walk_first;
+    const long long late_hint = h && h[4] >= 0 && h[0] >= 0 && h[5] >= 0 ? (long long)h[4] + h[0] + (halves ? h[5] : 0) : -1;
     const long long cap = c->late_cap > 0 ? c->late_cap
-                        : std::min<long long>((long long)P, late_hint >= 0 ? std::max(1ll << 16, 2 * late_hint)
-                                                                           : std::max<long long>(1 << 16, P / 4));
+                        : std::min<long long>((long long)P, std::max(1ll << 16, 2 * std::max(0ll, late_hint)));
     if ((r = d0.b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
     if ((r = c->g_old.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;
     if ((r = c->b_late.ensure(sizeof(RtLate) * (size_t)cap + 16)) != RT_OK) return r;
     if (!c->copy) HIP_TRY(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
     if (!c->ev_l0) HIP_TRY(hipEventCreateWithFlags(&c->ev_l0, hipEventDisableTiming));
+    // level 0's walk in two halves of tile rows (the first half's rows go down while the second runs)
+    const int tiles_x = (W + 7) / 8, tiles_y = (H + 7) / 8;
+    const bool split = halves && tiles_y >= 2;
+    const int R1 = split ? (tiles_y / 2) * 8 : H;
+    if (split) {
+        if (!c->aux) HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        for (hipEvent_t *e : {&c->ev_fs, &c->ev_h1, &c->ev_h2})
+            if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        L.aux_stream = c->aux;
+        L.ev_fs = c->ev_fs;
+        L.ev_h1 = c->ev_h1;
+        L.ev_h2 = c->ev_h2;
+        L.l0_split_tile = tiles_x * (tiles_y / 2);
+    }
     if (!c->h_info) HIP_TRY(hipHostMalloc((void **)&c->h_info, 2 * sizeof(int32_t), hipHostMallocDefault));
     float *f_rgb = (float *)d0.b_rgb.p, *old = (float *)c->g_old.p;
     RtLate *late = (RtLate *)c->b_late.p;
@@ -1048,11 +1083,23 @@ static int trace_frame_stream(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     // the copy stream: the previous values up (they are read before the level-0 result overwrites the
     // host buffer: same stream), then, once level 0 is shaded, the frame down
     if (!blend) HIP_TRY(hipMemcpyAsync(old, rgb_inout, sizeof(float) * 3 * P, hipMemcpyHostToDevice, Cs));
-    HIP_TRY(hipStreamWaitEvent(Cs, c->ev_l0, 0));
-    HIP_TRY(hipMemcpyAsync(rgb_inout, f_rgb, sizeof(float) * 3 * P, hipMemcpyDeviceToHost, Cs));
-    if (hit_entity) HIP_TRY(hipMemcpyAsync(hit_entity, L.hit_entity, sizeof(int32_t) * P, hipMemcpyDeviceToHost, Cs));
-    if (hit_node) HIP_TRY(hipMemcpyAsync(hit_node, L.hit_node, sizeof(int32_t) * P, hipMemcpyDeviceToHost, Cs));
-    if (status) HIP_TRY(hipMemcpyAsync(status, L.status, P, hipMemcpyDeviceToHost, Cs));
+    // rows [r0, r1) down once event `e` has passed
+    auto rows_down = [&](hipEvent_t e, int r0, int r1) -> int {
+        if (r1 <= r0) return RT_OK;
+        const size_t o = (size_t)r0 * W, n = (size_t)(r1 - r0) * W;
+        HIP_TRY(hipStreamWaitEvent(Cs, e, 0));
+        HIP_TRY(hipMemcpyAsync(rgb_inout + 3 * o, f_rgb + 3 * o, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, Cs));
+        if (hit_entity) HIP_TRY(hipMemcpyAsync(hit_entity + o, L.hit_entity + o, sizeof(int32_t) * n, hipMemcpyDeviceToHost, Cs));
+        if (hit_node) HIP_TRY(hipMemcpyAsync(hit_node + o, L.hit_node + o, sizeof(int32_t) * n, hipMemcpyDeviceToHost, Cs));
+        if (status) HIP_TRY(hipMemcpyAsync(status + o, L.status + o, n, hipMemcpyDeviceToHost, Cs));
+        return RT_OK;
+    };
+    if (split) {
+        if ((r = rows_down(c->ev_h1, 0, R1)) != RT_OK) return r;
+        if ((r = rows_down(c->ev_h2, R1, H)) != RT_OK) return r;
+    } else if ((r = rows_down(c->ev_l0, 0, H)) != RT_OK) {
+        return r;
+    }
     HIP_TRY(hipEventSynchronize(d0.sync));
     HIP_TRY(hipStreamSynchronize(Cs));
     *done = true;
@@ -1200,12 +1247,14 @@ extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     const size_t P = (size_t)W * (size_t)H;
     const bool blend = cfg->col_weight != 1.0;
     FrameOut o = {};
+    bool no_hint = false;
     if (c->gather == RT_GATHER_NONE && !stats && c->host_stream && c->split && (int64_t)P >= c->stream_min) {
         bool done = false;
-        r = trace_frame_stream(c, cam, cfg, rgb_inout, hit_entity, hit_node, status, &done);
+        r = trace_frame_stream(c, cam, cfg, rgb_inout, hit_entity, hit_node, status, &done, &no_hint);
         if (r != RT_OK || done) return r;
     }
-    if (c->gather == RT_GATHER_NONE && !stats && c->bands > 1 && c->split && H >= 16 && (int64_t)P >= c->band_min)
+    if (c->gather == RT_GATHER_NONE && !stats && !no_hint && c->bands > 1 && c->split && H >= 16 &&
+        (int64_t)P >= c->band_min)
         return trace_frame_bands(c, cam, cfg, rgb_inout, hit_entity, hit_node, status, c->bands);
     if (c->gather != RT_GATHER_NONE && !stats && c->host_direct)
         return trace_frame_parts_host(c, cam, cfg, rgb_inout, hit_entity, hit_node, status);

@@ -229,6 +229,11 @@ struct RtLaunch {
     int32_t late_cap;
     int32_t late_write;
     void *l0_done;
+    // ... and, with aux_stream, level 0's walk in two halves of tiles (split at l0_split_tile): half 1
+    // on the frame's stream, half 2 on aux_stream after ev_fs (frame start); ev_h1 / ev_h2 mark their
+    // ends (hipEvent_t).  l0_half is set per launch (0: all tiles)
+    void *aux_stream, *ev_fs, *ev_h1, *ev_h2;
+    int32_t l0_split_tile, l0_half;
     const int32_t *ctr_hint;                    // host snapshot of a recent frame's ctr (-1: none yet), or null
     int32_t *ctr_out;                           // pinned: this frame's ctr is copied here at its end (or null)
     void *ctr_done;                             // hipEvent_t recorded after that copy

@@ -2334,7 +2334,13 @@ __global__ void __launch_bounds__(BS, MINW) k_walk_first(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
-    const int items = n_items(L);
+    // a streamed host frame's level 0 in two launches (L.l0_half 1 / 2: the tiles before / from
+    // L.l0_split_tile, each with its own claim head), so that the first half's rows go to the host
+    // while the second half runs (rt_api.hip trace_frame_stream)
+    int items = n_items(L), t_base = 0;
+    int32_t *head = pass_heads(L, L.level, 1);
+    if (L.l0_half == 1) items = L.l0_split_tile;
+    if (L.l0_half == 2) { t_base = L.l0_split_tile; items -= t_base; head += 1; }
     const RtFrameSetup F = *L.setup;
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
@@ -2342,8 +2348,9 @@ __global__ void __launch_bounds__(BS, MINW) k_walk_first(RtLaunch L)
     stage_top(S);
     for (;;) {
         int t_end;
-        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
+        int t = claim_xcd(head, items, lane, 1, t_end, (L.xcd_mask & 1) && !L.l0_half);
         if (t >= items) break;
+        t += t_base;
         RaySrc src;
         ray_src(L, t, lane, src);
         if (!src.valid) continue;
@@ -2656,8 +2663,27 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             if (L.walk_first && lv == 0) {
                 // one wave per block: a part of an 8-GPU frame gives each wave about one tile, and a
                 // 4-wave block would hold its SIMD slots until its slowest tile ends
-                if (L.l0_bs == 64) launch_persistent(k_walk_first<4, 64>, st, Lw, mb, lds, 64);
-                else launch_persistent(k_walk_first<4>, st, Lw, mb, lds);
+                void (*kw)(RtLaunch) = L.l0_bs == 64 ? k_walk_first<4, 64> : k_walk_first<4>;
+                const int bs = L.l0_bs == 64 ? 64 : 256;
+                Lw.late_write = 0;
+                if (L.aux_stream && L.l0_split_tile > 0) {
+                    // two halves on two streams: the second fills the first's tail; each half's end
+                    // is an event for the host copy (trace_frame_stream)
+                    hipStream_t aux = (hipStream_t)L.aux_stream;
+                    HIP_TRY(hipEventRecord((hipEvent_t)L.ev_fs, st));
+                    RtLaunch L1 = Lw, L2 = Lw;
+                    L1.l0_half = 1;
+                    L2.l0_half = 2;
+                    launch_persistent(kw, st, L1, mb, lds, bs);
+                    HIP_TRY(hipEventRecord((hipEvent_t)L.ev_h1, st));
+                    HIP_TRY(hipStreamWaitEvent(aux, (hipEvent_t)L.ev_fs, 0));
+                    launch_persistent(kw, aux, L2, mb, lds, bs);
+                    HIP_TRY(hipEventRecord((hipEvent_t)L.ev_h2, aux));
+                    HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)L.ev_h2, 0));
+                    Lv.late_write = 1;            // level 0's shading writes after the halves went out
+                } else {
+                    launch_persistent(kw, st, Lw, mb, lds, bs);
+                }
             }
             else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb_plain, lds);
             HIP_TRY(hipGetLastError());

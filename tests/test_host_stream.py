@@ -25,8 +25,13 @@ def _same(a, b, ids=True):
     assert a["rc"] == b["rc"]
 
 
-def _ctx(scene, monkeypatch, stream, cap=None):
+FORCE = 1 << 24            # RT_LATE_CAP: stream every frame (the default streams only after a frame with
+                           # few late pixels), with room for every pixel
+
+
+def _ctx(scene, monkeypatch, stream, cap=FORCE, split="1"):
     monkeypatch.setenv("RT_HOST_STREAM", "1" if stream else "0")
+    monkeypatch.setenv("RT_STREAM_SPLIT", split)
     monkeypatch.setenv("RT_STREAM_MIN", "0")
     monkeypatch.setenv("RT_BANDS", "1")
     if cap:
@@ -44,15 +49,19 @@ def small3():
     return spec, rtamd.build_scene(spec)
 
 
-@pytest.mark.parametrize("cap", [None, 5])
-@pytest.mark.parametrize("wh", [(160, 120), (101, 37), (33, 200)])
-def test_streamed_equals_one_launch(small3, wh, cap, monkeypatch):
-    """Ids on and off, a second and third frame (late-list capacity from the grid hints), and a blend;
-    cap 5: the late list overflows and the frame is copied again whole."""
+@pytest.mark.parametrize("split", ["1", "0"])
+@pytest.mark.parametrize("cap", [None, FORCE, 5])
+@pytest.mark.parametrize("wh", [(160, 120), (101, 37), (33, 200), (64, 8)])
+def test_streamed_equals_one_launch(small3, wh, cap, split, monkeypatch):
+    """Ids on and off, a second and third frame, and a blend; cap None: the default choice (no stream
+    before a frame has counted its late pixels, then streamed if they are few), FORCE: every frame
+    streamed, 5: the late list overflows and the frame is copied again whole; split 1: level 0's walk
+    in two halves of tile rows on two streams, each half's rows sent when it ends (64x8: one tile row,
+    no split)."""
     spec, scene = small3
     cam, cfg = scenes.make_camera(*wh), scenes.make_config(3)
     one = _ctx(scene, monkeypatch, False)
-    st = _ctx(scene, monkeypatch, True, cap)
+    st = _ctx(scene, monkeypatch, True, cap, split)
     try:
         ref = one.trace_frame(cam, cfg, stats=False, allow_fault=True)
         for _ in range(3):
