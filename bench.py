@@ -562,7 +562,8 @@ def host_frame_time(ctx, cam, cfg, segments, scene=None, device=0, warm=3, reps=
     P = cam.width * cam.height
     streamed = os.environ.get("RT_HOST_STREAM", "1") != "0" and P >= int(os.environ.get("RT_STREAM_MIN", str(1 << 20)))
     out = dict(entry="rt_trace_frame (host RGB buffer, D2H included)", warmup=warm, frames=reps,
-               path="streamed after level 0" if streamed else "row bands / one launch",
+               path=("streamed after level 0 in two halves when a recent frame left few late pixels, else one launch"
+                     if streamed else "row bands / one launch"),
                ms_per_frame_median=round(med, 3), ms_min=round(min(ts), 3), ms_max=round(max(ts), 3),
                value=round(segments / (med * 1e-3) / 1e6, 3), unit="Mrays/s")
     if scene is not None:
