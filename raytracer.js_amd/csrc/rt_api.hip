@@ -463,6 +463,15 @@ extern "C" int rt_apply_edit(rt_ctx *c, const rt_edit_desc *d, rt_update_stats *
             if (d->rec_child[8 * k + j] < -1 || d->rec_child[8 * k + j] >= d->n_slots) return bad("rec_child", sl);
         if (d->rec_up[2 * k] < -1 || d->rec_up[2 * k] >= d->n_slots) return bad("rec_up", sl);
     }
+    {
+        // every new slot needs its record: apply_edit value-initialises new nodes (child[] = 0, the
+        // root), and a walk into one would cycle.  rec_slot is ascending and unique, so the records at
+        // slots >= n_nodes cover [n_nodes, n_slots) exactly when there are n_slots - n_nodes of them
+        // (this also bounds the growth by n_rec)
+        long long fresh = 0;
+        for (int k = 0; k < d->n_rec; k++) fresh += d->rec_slot[k] >= S0.n_nodes;
+        if (fresh != (long long)d->n_slots - S0.n_nodes) return bad("new slots without a record; n_slots", d->n_slots);
+    }
     e.rec_slot.assign(d->rec_slot, d->rec_slot + d->n_rec);
     e.rec_cube.assign(d->rec_cube, d->rec_cube + 4 * (size_t)d->n_rec);
     e.rec_child.assign(d->rec_child, d->rec_child + 8 * (size_t)d->n_rec);
@@ -491,8 +500,11 @@ extern "C" int rt_apply_edit(rt_ctx *c, const rt_edit_desc *d, rt_update_stats *
     e.sub_val.assign(d->sub_val, d->sub_val + d->n_sub);
     for (int i = 0; i < d->n_dfs_new; i++)
         if (d->dfs_new_slot[i] < S0.n_nodes || d->dfs_new_slot[i] >= d->n_slots) return bad("dfs_new_slot", d->dfs_new_slot[i]);
-    for (int i = 1; i < d->n_dfs_shift; i++)
-        if (d->dfs_shift[i] < d->dfs_shift[i - 1]) return bad("dfs_shift (ascending)", i);
+        else if (d->dfs_new_val[i] < 0 || d->dfs_new_val[i] >= d->n_slots) return bad("dfs_new_val", d->dfs_new_val[i]);
+    if (d->n_dfs_shift > d->n_slots) return bad("n_dfs_shift", d->n_dfs_shift);
+    for (int i = 0; i < d->n_dfs_shift; i++)
+        if (d->dfs_shift[i] < 0 || d->dfs_shift[i] > d->n_slots || (i && d->dfs_shift[i] < d->dfs_shift[i - 1]))
+            return bad("dfs_shift (ascending, in [0, n_slots])", i);
     e.dfs_new_slot.assign(d->dfs_new_slot, d->dfs_new_slot + d->n_dfs_new);
     e.dfs_new_val.assign(d->dfs_new_val, d->dfs_new_val + d->n_dfs_new);
     e.dfs_shift.assign(d->dfs_shift, d->dfs_shift + d->n_dfs_shift);
@@ -585,11 +597,16 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
                 hipEventCreateWithFlags(&d.ctr_ev[1], hipEventDisableTiming) != hipSuccess)
                 return rt_set_error(RT_E_HIP, "prepare: grid-hint buffers");
             d.ctr_snap.assign(RT_CTR_INTS, -1);                             // unknown until a frame completes
+            std::fill(d.h_ctr, d.h_ctr + 2 * RT_CTR_INTS, -1);
         }
+        // a frame that took a buffer but sent no counters (fused small frame, empty part, an error
+        // before the copy) never records its event, and the query then reports success: the buffer
+        // still holds the -1 it was given below (a copied ctr[0], the overflow count, is >= 0), and
+        // the snapshot keeps the last real counts
         for (int i = 0; i < 2; i++)
             if (d.ctr_pend[i] && hipEventQuery(d.ctr_ev[i]) == hipSuccess) {
                 d.ctr_pend[i] = false;
-                if (d.ctr_seq[i] > d.ctr_snap_seq) {
+                if (d.ctr_seq[i] > d.ctr_snap_seq && d.h_ctr[(size_t)i * RT_CTR_INTS] >= 0) {
                     memcpy(d.ctr_snap.data(), d.h_ctr + (size_t)i * RT_CTR_INTS, sizeof(int32_t) * RT_CTR_INTS);
                     d.ctr_snap_seq = d.ctr_seq[i];
                 }
@@ -603,6 +620,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
             const int w = !d.ctr_pend[0] ? 0 : 1;
             d.ctr_pend[w] = true;
             d.ctr_seq[w] = ++d.ctr_frames;
+            d.h_ctr[(size_t)w * RT_CTR_INTS] = -1;                           // no transfer in flight to it
             L.ctr_out = d.h_ctr + (size_t)w * RT_CTR_INTS;
             L.ctr_done = d.ctr_ev[w];
         }

@@ -1165,6 +1165,9 @@ __device__ __forceinline__ int wave_min(int v)
 // at most H/2 + W/2 steps of one multiply-add pair, bit-identical to the sequential scan.
 // dirs: SoA planes [3][W*rows], x-major (index x*rows + local row): a wave stores 64 consecutive
 // rows of one column per step, and an 8x8 tile of the walk reads 8 runs of 64 bytes per plane.
+typedef unsigned int rt_u32x2 __attribute__((ext_vector_type(2)));
+#define RT_BUFFER_DWORD3 0x00020000             // gfx9 raw buffer: 32-bit data format, no swizzle
+
 __device__ __forceinline__ void rotate_1(double &x, double &y, double c, double s)
 {
     const double nx = x * c + y * s, ny = x * -s + y * c;      // rotate_vectors, one component
@@ -1172,7 +1175,7 @@ __device__ __forceinline__ void rotate_1(double &x, double &y, double c, double 
     y = ny;
 }
 
-__global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
+__global__ void __launch_bounds__(64) k_frame_start(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
                                                      RtFrameSetup *setup, int part, int n_parts, int stripe,
                                                      int rows, int row0, double *__restrict__ dirs, int32_t *ctr,
                                                      int32_t *fault, int tl)
@@ -1212,9 +1215,14 @@ __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_des
         }
         return;
     }
-    const int t = (blockIdx.x - 1) * blockDim.x + threadIdx.x;
-    if (t >= 6 * rows) return;
-    const int lr = t % rows, hc = t / rows;
+    // block b >= 1 is one wave: (component, half) is uniform over it and its lanes are 64 consecutive
+    // local rows, so the horizontal chain's rotation constants and its store column live in scalar
+    // registers and a step's store is one global_store with a scalar base (no per-lane address math)
+    const int wpg = (rows + 63) >> 6;                 // waves per (component, half)
+    const int hc = (int)(blockIdx.x - 1) / wpg;
+    if (hc >= 6) return;
+    const int lr0 = ((int)(blockIdx.x - 1) - hc * wpg) << 6, lr = lr0 + (int)threadIdx.x;
+    if (lr >= rows) return;
     const int i = hc >> 1;                    // component
     const bool right = (hc & 1) == 0;
     const int W = cam.width, H = cam.height;
@@ -1239,13 +1247,31 @@ __global__ void __launch_bounds__(256) k_frame_start(RtDevScene S, rt_camera_des
     double l = cam.lf[i];
     if (!right) rotate_1(f, l, c, sh);
     const int from = right ? (W >> 1) : (W >> 1) - 1, inc = right ? 1 : -1;
-    double *p = dirs + (size_t)i * (size_t)rows * (size_t)W + (size_t)from * (size_t)rows + (size_t)lr;
-    const ptrdiff_t step = (ptrdiff_t)inc * (ptrdiff_t)rows;
     const int n = right ? W - from : from + 1;
+    // the component's plane as a buffer resource: a step's store is buffer_store with the lane's row
+    // as its vector offset and the column in a scalar offset, stepped by scalar adds (no per-lane
+    // address arithmetic in the chain's loop); the plane's size bounds every store.  A plane of
+    // 2 GiB or more (over 2^28 pixels in the part) takes 64-bit pointers
+    const size_t plane_sz = (size_t)rows * (size_t)W * sizeof(double);
+    if (plane_sz >= ((size_t)1 << 31)) {
+        double *p = dirs + (size_t)i * (size_t)rows * (size_t)W + (size_t)from * (size_t)rows + (size_t)lr;
+        const ptrdiff_t step = (ptrdiff_t)inc * (ptrdiff_t)rows;
+        for (int k = 0; k < n; k++) {
+            *p = f;
+            p += step;
+            rotate_1(f, l, c, sh);
+        }
+        return;
+    }
+    const int plane_bytes = (int)plane_sz;
+    const __amdgpu_buffer_rsrc_t plane = __builtin_amdgcn_make_buffer_rsrc(
+        dirs + (size_t)i * (size_t)rows * (size_t)W, 0, plane_bytes, RT_BUFFER_DWORD3);
+    const int voff = lr * (int)sizeof(double), sstep = inc * rows * (int)sizeof(double);
+    int soff = from * rows * (int)sizeof(double);
 #pragma unroll 4
     for (int k = 0; k < n; k++) {
-        *p = f;
-        p += step;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(rt_u32x2, f), plane, voff, soff, 0);
+        soff += sstep;
         rotate_1(f, l, c, sh);
     }
 }
@@ -2579,10 +2605,12 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
 {
     hipStream_t st = (hipStream_t)stream;
     const int W = L.cam.width;
-    const int rg_lanes = 6 * (L.rows > 0 ? L.rows : 0);
     (void)hipGetLastError();                     // a stale error of an earlier runtime call is not ours
     const bool trace = L.rows > 0 && !L.skip_trace;
-    hipLaunchKernelGGL(k_frame_start, dim3(1 + (rg_lanes + 255) / 256), dim3(256), 0, st, L.scene, L.cam, L.cfg,
+    // one wave per block (6 per row band of 64), so that the ~100 chain waves of a 1080p frame land
+    // on ~100 CUs: a chain step with its store costs 64 cycles with 4 such waves on a CU against 48
+    // alone (tools/probe/chain_latency.hip)
+    hipLaunchKernelGGL(k_frame_start, dim3(1 + 6 * ((std::max(L.rows, 0) + 63) / 64)), dim3(64), 0, st, L.scene, L.cam, L.cfg,
                        L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.row0, L.dirs, trace ? L.ctr : nullptr,
                        L.zero_fault ? L.fault : nullptr,
                        tl_next(reinterpret_cast<const void *>(k_frame_start), st));
