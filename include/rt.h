@@ -32,10 +32,11 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4   /* 2: rt_config_desc gained scatter_seed / scatter_mode;
+#define RT_ABI_VERSION 5   /* 2: rt_config_desc gained scatter_seed / scatter_mode;
                               3: image textures (rt_image_desc, rt_shade.image, sky_image);
                               4: multi-device contexts (rt_create_desc.devices), rt_trace_frame_device,
-                                 rt_frame_fault, rt_ctx_info */
+                                 rt_frame_fault, rt_ctx_info;
+                              5: rt_set_lights (shadow rays, a build extension) */
 #define RT_MAX_DEVICES 8
 
 /* ---- return codes ---------------------------------------------------------------------- */
@@ -299,6 +300,30 @@ int  rt_trace_frame_device(rt_ctx *ctx, const rt_camera_desc *cam, const rt_conf
  * (rt_trace_frame_device / rt_trace_rows_device) reached a reference throw (RT_E_FAULT of
  * rt_trace_frame), else 0. */
 int  rt_frame_fault(rt_ctx *ctx, int32_t *fault);
+
+/* Shadow rays: a BUILD EXTENSION, off by default (the reference samples no lights,
+ * src/raytracer.ts:168-277; BASELINE config 5 names "shadow rays").  Frozen definition (DESIGN.md
+ * §3.7; the oracle's orc_set_lights implements the same): with n > 0 point lights, a ray that ends on
+ * a matte surface (REFLECTION, not a mirror, not a light), after alter_ray and the path-length update,
+ * at point p with the hit normal nrm and path length `path`, multiplies its colour channel-wise by
+ *     s = ambient + sum over lights l (in order) of  rgb_l * (cosine * isl)
+ * where, in binary64 without contraction and in this order: v = pos_l - p; dist = sqrt(v.v) (skip the
+ * light unless dist > 0); u = v * (1/dist); cosine = nrm.u (skip unless cosine > 0); the shadow ray
+ * starts at q = p + u*1e-3 (move_slightly_forward), is seated like a continuation
+ * (set_pos_and_dir without a node) and walked in the reference's walker order, each node's Set in
+ * order; its FIRST hit decides: the light is blocked when that hit's entity is not a light and
+ * |hit - q| < dist - 1e-3, or when the seat or the walk throws or reaches the step cap; otherwise
+ * t = (path + dist) * distance_attenuation_factor and isl = 1/(EPSILON + t*t) (the reference's
+ * inverse-square law, src/raytracer.ts:274-275).  Shadow-ray tests are not counted in rt_stats, and
+ * hit ids / status stay those of the primary ray.  n = 0 (the default) restores the reference's
+ * behaviour bit for bit.  Frames with lights run the fused one-kernel path.  Applies to the
+ * context's later frames; not while a frame of the context is in flight. */
+#define RT_MAX_LIGHTS 4
+typedef struct rt_light {
+    double pos[3];
+    double rgb[3];
+} rt_light;
+int  rt_set_lights(rt_ctx *ctx, const rt_light *lights, int32_t n, double ambient);
 
 /* Kernel time (ms) of the last `n` trace-kernel launches issued by rt_trace_rows_device, oldest
  * first, measured with HIP events on the launch stream.  Synchronises.  Returns count written. */

@@ -51,6 +51,7 @@ def lib():
     L.orc_walker_set.argtypes = [vp, pd, pd, vp, i]
     L.orc_walker_next.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_int)]
     L.orc_set_tables.argtypes = [vp, C.POINTER(abi.rt_shade), i, pd, i]
+    L.orc_set_lights.argtypes = [vp, C.POINTER(abi.rt_light), i, C.c_double]
     L.orc_add_entity.argtypes = [vp, vp, i, pd, i, i, i, i, C.POINTER(vp)]
     L.orc_entity_in_set.argtypes = [vp, i]
     L.orc_entity_at_pos.argtypes = [vp, vp, pd]
@@ -172,6 +173,14 @@ class World:
         self._shades, self._ri = shades, ri
         self.L.orc_set_tables(self.h, shades.ctypes.data_as(C.POINTER(abi.rt_shade)), len(shades),
                               ri.ctypes.data_as(C.POINTER(C.c_double)), len(ri))
+
+    def set_lights(self, lights, ambient=0.0):
+        """Shadow rays (a build extension, include/rt.h rt_set_lights): [(pos, rgb), ...], at most
+        RT_MAX_LIGHTS; [] restores the reference."""
+        arr = abi.lights_array(lights)
+        r = self.L.orc_set_lights(self.h, arr, len(lights), float(ambient))
+        if r != 0:
+            raise ValueError("orc_set_lights: %d" % r)
 
     def set_images(self, images):
         """ImageTextures, [H, W, 3] uint8 each (copied by the oracle)."""

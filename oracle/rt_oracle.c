@@ -115,6 +115,9 @@ struct oworld {
     int n_ri;
     rt_image_desc *images;   /* ImageTextures (each rgb a private copy) */
     int n_images;
+    int n_lights;            /* shadow rays (build extension, orc_set_lights): 0 = the reference */
+    double ambient;
+    rt_light lights[RT_MAX_LIGHTS];
 };
 
 oworld *orc_world_new(void)
@@ -1208,8 +1211,76 @@ uint32_t orc_scatter_dir(uint64_t seed, uint64_t pixel, uint32_t draws, const do
 
 double orc_counter_draw_at(uint64_t seed, uint64_t pixel, uint32_t n) { return orc_counter_draw(seed, pixel, n); }
 
-static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], uint64_t pixel, ray_out *ro)
+/* ---- shadow rays: a BUILD EXTENSION (the reference samples no lights, src/raytracer.ts:168-277).
+ * The frozen definition is include/rt.h's rt_set_lights comment; this is its CPU
+ * statement, the GPU's parity target.  Not pinned by any reference output: parity is against this. */
+int orc_set_lights(oworld *w, const rt_light *lights, int n, double ambient)
 {
+    if (n < 0 || n > RT_MAX_LIGHTS || (n && !lights)) return RT_E_INVALID;
+    w->n_lights = n;
+    w->ambient = n ? ambient : 0;
+    for (int k = 0; k < n; k++) w->lights[k] = lights[k];
+    return 0;
+}
+
+/* 1 when the shadow ray (q, u) is blocked before dist: its first hit in walk order (Set order within
+ * a node) decides; a throw or the step cap blocks.  wks: a walker whose counters nobody reads. */
+static int shadow_blocked(oworld *w, owalker *wks, const double q[3], const double u[3], double dist)
+{
+    if (orc_walker_set(wks, q, u, NULL, 0) < 0) return 1;
+    for (;;) {
+        onode *node, *pt;
+        int po;
+        int r = orc_walker_next(wks, &node, &pt, &po);
+        if (r < 0) return 1;
+        if (r == 0) return 0;
+        int hit_id = -1;
+        ohit h;
+        for (int i = 0; i < node->set_n; i++) {
+            const oentity *e = &w->ents[node->set[i]];
+            memset(&h, 0, sizeof h);
+            int got;
+            if (e->type == RT_ENT_SPHERE) got = sphere_collision(e, q, u, &h);
+            else if (e->type == RT_ENT_BOX) got = box_collision(e, q, u, &h);
+            else got = face_collision(e, q, u, &h);
+            if (got) { hit_id = node->set[i]; break; }
+        }
+        if (hit_id < 0) continue;
+        if (h.fault) return 1;
+        if (w->shades[w->ents[hit_id].shade].light) return 0;
+        double diff[3] = {h.point[0] - q[0], h.point[1] - q[1], h.point[2] - q[2]};
+        return sqrt(vdot(diff, diff)) < dist - 1e-3;
+    }
+}
+
+/* the matte hit's light factor: ambient + the unblocked lights' rgb * (cosine * isl) */
+static void shadow_factor(oworld *w, owalker *wks, const rt_config_desc *cfg, const double p[3],
+                          const double nrm[3], double path, double s[3])
+{
+    s[0] = s[1] = s[2] = w->ambient;
+    for (int l = 0; l < w->n_lights; l++) {
+        const rt_light *lt = &w->lights[l];
+        double v[3] = {lt->pos[0] - p[0], lt->pos[1] - p[1], lt->pos[2] - p[2]};
+        double dist = sqrt(vdot(v, v));
+        if (!(dist > 0)) continue;
+        double inv = 1.0 / dist;
+        double u[3] = {v[0] * inv, v[1] * inv, v[2] * inv};
+        double cosine = vdot(nrm, u);
+        if (!(cosine > 0)) continue;
+        double q[3] = {p[0] + u[0] * 1e-3, p[1] + u[1] * 1e-3, p[2] + u[2] * 1e-3};
+        if (shadow_blocked(w, wks, q, u, dist)) continue;
+        double t = (path + dist) * cfg->distance_attenuation_factor;
+        double isl = 1.0 / (2.220446049250313e-16 + t * t);
+        double k = cosine * isl;
+        for (int i = 0; i < 3; i++) s[i] += lt->rgb[i] * k;
+    }
+}
+
+static void trace_ray(const trace_ctx *tc, owalker *wk, owalker *wks, const double dir0[3], uint64_t pixel,
+                      ray_out *ro)
+{
+    int matte = 0;                                                           /* shadow rays */
+    double mnrm[3] = {0, 0, 0};
     uint32_t draws = 0;
     oworld *w = tc->w;
     const rt_config_desc *cfg = tc->cfg;
@@ -1269,7 +1340,10 @@ static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], ui
         o[0] = h.point[0]; o[1] = h.point[1]; o[2] = h.point[2];
         if (sh->light) { light_hit = 1; break; }
         if (sh->response == RT_RESP_REFLECTION) {
-            if (!sh->mirror) goto out;                          /* matte: terminal */
+            if (!sh->mirror) {                                  /* matte: terminal */
+                if (w->n_lights) { matte = 1; mnrm[0] = h.normal[0]; mnrm[1] = h.normal[1]; mnrm[2] = h.normal[2]; }
+                goto out;
+            }
             /* reflect_ray → vector.reflection (src/math/vector.ts:263-268) */
             double ns = -vdot(d, h.normal);
             double k = ns * 2;
@@ -1332,6 +1406,11 @@ static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], ui
         if (orc_walker_set(wk, o, d, NULL, 0) < 0) ro->status = ST_FAULT;
     }
 out:
+    if (matte) {
+        double sf[3];
+        shadow_factor(w, wks, cfg, o, mnrm, path, sf);
+        for (int i = 0; i < 3; i++) col[i] = col[i] * sf[i];
+    }
     ro->rgb[0] = col[0]; ro->rgb[1] = col[1]; ro->rgb[2] = col[2];
 }
 
@@ -1347,7 +1426,7 @@ typedef struct frame_job {
     int32_t *hit_entity, *hit_node, *segs;
     uint8_t *status;
     int tid, nthreads;
-    owalker *wk;
+    owalker *wk, *wks;      /* wks: shadow rays' walker (its counters are not reported) */
     int64_t counters[11];
 } frame_job;
 
@@ -1360,7 +1439,7 @@ static void *frame_worker(void *arg)
         int p = j->pix ? j->pix[k] : k;
         ray_out ro;
         memset(&ro, 0, sizeof ro);
-        trace_ray(j->tc, j->wk, j->dirs + 3 * (size_t)p, (uint64_t)p, &ro);
+        trace_ray(j->tc, j->wk, j->wks, j->dirs + 3 * (size_t)p, (uint64_t)p, &ro);
         /* ExposureBuffer.set_color_i — src/view/exposure_buffer.ts:77-91 */
         float *px = j->rgb + 3 * (size_t)p;
         for (int c = 0; c < 3; c++) {
@@ -1424,6 +1503,7 @@ int orc_trace_frame(oworld *w, onode *root, const rt_camera_desc *cam, const rt_
         j->rgb = rgb_inout; j->hit_entity = hit_entity; j->hit_node = hit_node; j->segs = segments;
         j->status = status; j->tid = t; j->nthreads = nthreads;
         j->wk = orc_walker_new(w, root, 0);
+        j->wks = orc_walker_new(w, root, 0);
     }
     if (nthreads == 1) frame_worker(&jobs[0]);
     else {

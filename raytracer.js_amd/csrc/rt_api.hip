@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <array>
 #include <chrono>
 #include <new>
@@ -81,7 +82,8 @@ struct RtDevice {
     hipStream_t stream = nullptr;
     RtDevScene scene{};
     DevBuf b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters,
-        b_fault;
+        b_fault, b_lights;
+    uint64_t lights_seq = 0;                     // the rt_set_lights call b_lights holds
     std::vector<std::array<hipEvent_t, 2>> ev;   // trace-kernel timing ring
     int ev_next = 0, ev_count = 0;
     hipEvent_t sync = nullptr;                   // cross-stream / cross-device ordering
@@ -101,6 +103,10 @@ struct rt_ctx {
     int flags = 0;
     bool bvh_sah = true;             // SAH splits (RT_BVH_SAH=0: median split)
     bool split = true;               // walk pass + test pass (RT_SPLIT=0: fused k_trace)
+    int n_lights = 0;                // rt_set_lights: shadow rays (a build extension; 0 = off)
+    double ambient = 0;
+    rt_light lights[RT_MAX_LIGHTS] = {};
+    uint64_t lights_seq = 0;         // bumped per rt_set_lights; a device uploads at its next frame
     int cand_cap = 64;               // candidate nodes per pixel in the split path (RT_CAND_CAP)
     int split_levels = RT_MAX_LEVELS + 1;   // split-path bounce levels (RT_SPLIT_LEVELS)
     int claim_chunk = 1;             // items per queue claim in the short passes (RT_CLAIM_CHUNK)
@@ -177,7 +183,7 @@ static void release_device(RtDevice &d)
 {
     (void)hipSetDevice(d.device);
     for (DevBuf *b : {&d.b_cand, &d.b_cand_n, &d.b_first, &d.b_queue, &d.b_ctr, &d.b_setup, &d.b_dirs, &d.b_rgb,
-                      &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault})
+                      &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault, &d.b_lights})
         b->release();
     for (auto &e : d.ev)
         for (hipEvent_t x : e)
@@ -523,6 +529,21 @@ extern "C" int rt_apply_edit(rt_ctx *c, const rt_edit_desc *d, rt_update_stats *
     return RT_OK;
 }
 
+extern "C" int rt_set_lights(rt_ctx *c, const rt_light *lights, int32_t n, double ambient)
+{
+    if (!c || n < 0 || n > RT_MAX_LIGHTS || (n && !lights) || !std::isfinite(ambient))
+        return rt_set_error(RT_E_INVALID, "rt_set_lights: bad argument (n = %d, 0..%d)", n, RT_MAX_LIGHTS);
+    for (int k = 0; k < n; k++)
+        for (int i = 0; i < 3; i++)
+            if (!std::isfinite(lights[k].pos[i]) || !std::isfinite(lights[k].rgb[i]))
+                return rt_set_error(RT_E_INVALID, "rt_set_lights: light %d is not finite", k);
+    c->n_lights = n;
+    c->ambient = n ? ambient : 0;
+    for (int k = 0; k < RT_MAX_LIGHTS; k++) c->lights[k] = k < n ? lights[k] : rt_light{};
+    c->lights_seq++;
+    return RT_OK;
+}
+
 extern "C" int rt_scene_node_slots(rt_ctx *c, int32_t *out, int32_t n, int32_t *n_slots)
 {
     if (!c || !out || n < 0 || !n_slots) return rt_set_error(RT_E_INVALID, "rt_scene_node_slots: bad argument");
@@ -644,7 +665,17 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.level_solo = c->level_solo == 2 ? 2 : (c->level_solo && c->hints);
 
     L.blend = cfg->col_weight != 1.0;
-    if (c->split && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {
+    if (c->n_lights) {
+        if (d.lights_seq != c->lights_seq) {
+            if ((r = d.b_lights.ensure(sizeof(rt_light) * RT_MAX_LIGHTS)) != RT_OK) return r;
+            HIP_TRY(hipMemcpy(d.b_lights.p, c->lights, sizeof(rt_light) * RT_MAX_LIGHTS, hipMemcpyHostToDevice));
+            d.lights_seq = c->lights_seq;
+        }
+        L.n_lights = c->n_lights;
+        L.ambient = c->ambient;
+        L.lights = (const rt_light *)d.b_lights.p;
+    }
+    if (c->split && !c->n_lights && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).
         // the walk kernels address the lists with 32-bit byte offsets (cand_store): cand_cap * P * 4 < 2^32

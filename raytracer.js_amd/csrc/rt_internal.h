@@ -237,6 +237,11 @@ struct RtLaunch {
     const int32_t *ctr_hint;                    // host snapshot of a recent frame's ctr (-1: none yet), or null
     int32_t *ctr_out;                           // pinned: this frame's ctr is copied here at its end (or null)
     void *ctr_done;                             // hipEvent_t recorded after that copy
+    // shadow rays (rt_set_lights, include/rt.h): n_lights point lights in device memory, 0 = off (the
+    // fused path runs them)
+    int32_t n_lights;
+    double ambient;
+    const rt_light *lights;
 };
 
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };

@@ -322,7 +322,7 @@ __device__ int walker_setup(const RtDevScene &S, Walker &w)
 }
 
 // set_pos_and_dir(pos, dir, node?) — :188-226.  Returns 0 or -1 (throw).
-__device__ int walker_set(const RtDevScene &S, Walker &w, const double o[3], const double d[3],
+__device__ __forceinline__ int walker_set(const RtDevScene &S, Walker &w, const double o[3], const double d[3],
                           bool have_node, int tree, int oct, Counters &c)
 {
     w.d[0] = d[0]; w.d[1] = d[1]; w.d[2] = d[2];
@@ -513,7 +513,7 @@ __device__ __forceinline__ int walker_update_next_pos(const NodeDims &p, Walker 
 // STOP (segmented walks): return 2 instead of updating the empty slot
 // `stop` = tree * 8 + octant, i.e. when the walk arrives at the cell where the next segment starts.
 template <bool INCL_UNDEF, bool STOP = false>
-__device__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_tree, int &pos_oct, Counters &c,
+__device__ __forceinline__ int walker_next(const RtDevScene &S, Walker &w, int &node, int &pos_tree, int &pos_oct, Counters &c,
                            int stop = -1)
 {
     while (w.cur_tree >= 0) {
@@ -933,7 +933,7 @@ __device__ __forceinline__ bool prim_within(const RtPrim &pr, const double p[3])
 // Prims of a node are stored in cull order, so the first entity in Set order is the minimum rank.
 // Only the node's spheres and boxes are visited (S.within): a face's is_within is false, and the
 // sets of shallow nodes hold thousands of straddling triangles (config 5's path: ~2400 per lookup).
-__device__ int entity_at_pos(const RtDevScene &S, const double p[3], long long &levels)
+__device__ __forceinline__ int entity_at_pos(const RtDevScene &S, const double p[3], long long &levels)
 {
     int t = -1, oc = 0;
     const int r = node_at_pos(S, p, t, oc, levels);
@@ -1018,7 +1018,7 @@ __device__ __forceinline__ int prim_hit(const RtPrim &pr, const double o[3], con
 // exact hits (a throwing test counts as a hit: the loop reaches it only if nothing earlier hit).
 // Returns the prim slot or -1; *rank_out receives its rank.
 template <bool STATS>
-__device__ int node_first_hit(const RtDevScene &S, const int4 ne, const double o[3], const double d[3],
+__device__ __forceinline__ int node_first_hit(const RtDevScene &S, const int4 ne, const double o[3], const double d[3],
                               const RayBox &rb, bool cull, Counters &c, long long &box_ctr, Hit &h, int &rank_out,
                               bool root_hit = false)
 {
@@ -1376,6 +1376,74 @@ __device__ __forceinline__ void scatter_dir(uint64_t seed, uint64_t gpix, uint32
     d[0] = r0 * inv; d[1] = r1 * inv; d[2] = r2 * inv;
 }
 
+// The continuation queue of bounce level k (levels alternate between two).  A select, not an index:
+// a dynamic index into the by-value launch record makes the compiler copy the record to scratch.
+__device__ __forceinline__ RtCont *lvl_queue(const RtLaunch &L, int k)
+{
+    return (k & 1) ? L.queue[1] : L.queue[0];
+}
+
+// ---- shadow rays (a build extension, rt_set_lights; definition: include/rt.h) ----
+// Whether the shadow ray from q along u (unit) reaches a light at distance dist: its first hit in the
+// reference's walk order decides.  The work is not counted (cs is the caller's scratch).
+__device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, const double q[3], const double u[3], double dist,
+                               Counters &cs)
+{
+    Walker w;
+    if (walker_set(S, w, q, u, false, 0, 0, cs) < 0) return true;          // the seat throws
+    const RayBox rb = make_raybox(q, u);
+    for (;;) {
+        int node, pt, po;
+        const int r = walker_next<false>(S, w, node, pt, po, cs);
+        if (r < 0) return true;                                             // throw, step cap
+        if (r == 0) return false;
+        const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
+        if (ent.y == 0) continue;
+        Hit h;
+        int rank;
+        long long box = 0;
+        const int hk = node_first_hit<false>(S, ent, q, u, rb, cull, cs, box, h, rank);
+        if (hk < 0) continue;
+        const RtPrim &pr = S.prim[hk];
+        if (prim_hit(pr, q, u, h) < 0) return true;                         // the winner throws
+        if (S.shades[pr.meta >> 2].light) return false;
+        const double a = h.p[0] - q[0], b = h.p[1] - q[1], e = h.p[2] - q[2];
+        return sqrt(dot3(a, b, e, a, b, e)) < dist - 1e-3;
+    }
+}
+
+// The matte hit's light factor s (per channel): ambient + the unblocked lights' rgb * cosine * isl.
+__device__ __forceinline__ void shadow_factor(const RtDevScene &S, const RtLaunch &L, bool cull, const double p[3],
+                              const double nrm[3], double path, double s[3])
+{
+    Counters cs = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    s[0] = s[1] = s[2] = L.ambient;
+    for (int l = 0; l < L.n_lights; l++) {
+        const rt_light lt = L.lights[l];
+        const double v0 = lt.pos[0] - p[0], v1 = lt.pos[1] - p[1], v2 = lt.pos[2] - p[2];
+        const double dist = sqrt(dot3(v0, v1, v2, v0, v1, v2));
+        if (!(dist > 0)) continue;
+        const double inv = 1.0 / dist;
+        const double u[3] = {v0 * inv, v1 * inv, v2 * inv};
+        const double cosine = dot3(nrm[0], nrm[1], nrm[2], u[0], u[1], u[2]);
+        if (!(cosine > 0)) continue;
+        const double q[3] = {p[0] + u[0] * 1e-3, p[1] + u[1] * 1e-3, p[2] + u[2] * 1e-3};
+        if (shadow_blocked(S, cull, q, u, dist, cs)) continue;
+        const double t = (path + dist) * L.cfg.distance_attenuation_factor;
+        const double isl = 1.0 / (2.220446049250313e-16 + t * t);
+        const double k = cosine * isl;
+        s[0] += lt.rgb[0] * k;
+        s[1] += lt.rgb[1] * k;
+        s[2] += lt.rgb[2] * k;
+    }
+}
+
+template <bool SHADOW> struct MatteHit {
+    bool on = false;
+    double n[3];
+};
+template <> struct MatteHit<false> {};
+
 // Trace modes, all running the same bounce loop (src/raytracer.ts:168-277):
 //   TR_FUSED   walks every segment (state from the camera, or from record `rs`);
 //   TR_LIST    the first segment (primary ray, or the queued segment `rs`) was resolved by k_walk +
@@ -1386,8 +1454,8 @@ __device__ __forceinline__ void scatter_dir(uint64_t seed, uint64_t gpix, uint32
 // walker re-seat of src/raytracer.ts:254 is still to do).
 enum { TR_FUSED = 0, TR_LIST = 1 };
 
-template <bool STATS, int MODE>
-__device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg, bool cull,
+template <bool STATS, int MODE, bool SHADOW = false>
+__device__ __forceinline__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg, bool cull,
                           int diag, const double cam_pos[3], const double dir0[3], RayResult &R, Counters &c,
                           int cn, const ListHit &pre, const RtCont *rs, const RayQueues &Q, int pix,
                           const RtLaunch &L)
@@ -1402,6 +1470,7 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
     Walker w;
     bool seat = false;           // segment start: re-seat the walker at (o, d) (src/raytracer.ts:254)
     bool first_stop = true;      // TR_LIST: the resolved stop not yet consumed
+    MatteHit<SHADOW> matte;      // SHADOW: whether the ray ended on a matte surface, and its normal
     R.status = ST_OK;
     if (rs) {
         for (int i = 0; i < 3; i++) { o[i] = rs->o[i]; d[i] = rs->d[i]; }
@@ -1497,7 +1566,13 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         o[0] = h.p[0]; o[1] = h.p[1]; o[2] = h.p[2];
         if (sh.light) { light_hit = true; break; }
         if (sh.response == RT_RESP_REFLECTION) {
-            if (!sh.mirror) goto done;                          // matte: terminal
+            if (!sh.mirror) {                                   // matte: terminal
+                if constexpr (SHADOW) {                         // shadow rays after the walk (below)
+                    matte.on = true;
+                    matte.n[0] = h.n[0]; matte.n[1] = h.n[1]; matte.n[2] = h.n[2];
+                }
+                goto done;
+            }
             const double k2 = -dot3(d[0], d[1], d[2], h.n[0], h.n[1], h.n[2]) * 2;   // vector.reflection
             d[0] = d[0] + h.n[0] * k2; d[1] = d[1] + h.n[1] * k2; d[2] = d[2] + h.n[2] * k2;
             if (sh.roughness > 0.0) {                                                  // :233-235
@@ -1566,6 +1641,13 @@ __device__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_c
         if (walker_set(S, w, o, d, false, 0, 0, c) < 0) R.status = ST_FAULT;
     }
 done:
+    if constexpr (SHADOW) {
+        if (matte.on && L.n_lights > 0) {                       // shadow rays (rt_set_lights)
+            double sf[3];
+            shadow_factor(S, L, cull, o, matte.n, path, sf);
+            col0 = col0 * sf[0]; col1 = col1 * sf[1]; col2 = col2 * sf[2];
+        }
+    }
     R.rgb[0] = col0; R.rgb[1] = col1; R.rgb[2] = col2;
 }
 
@@ -1701,7 +1783,7 @@ __device__ __forceinline__ void ray_src(const RtLaunch &L, int item, int lane, R
         r.valid = lane < g && q < *lvl_ctr(L, L.level - 1);
         if (!r.valid) return;
         r.id = (size_t)q;
-        r.rec = L.queue[(L.level - 1) & 1] + q;
+        r.rec = lvl_queue(L, L.level - 1) + q;
         r.pix = r.rec->pix;
         for (int i = 0; i < 3; i++) { r.o[i] = r.rec->o[i]; r.d[i] = r.rec->d[i]; }
     }
@@ -1731,7 +1813,7 @@ __device__ __forceinline__ void pixel_src(const RtLaunch &L, int id, RaySrc &r)
 // orders of magnitude across the frame (rays that hit early vs rays that cross every upper-level
 // set), so wave-granular dynamic scheduling replaces the fixed block->tile mapping and its tail.
 // The fused kernel: the stats build, and the RT_CREATE_NO_SPLIT path.
-template <bool STATS, int MINW>
+template <bool STATS, int MINW, bool SHADOW = false>
 __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
 {
     TL_SCOPE(L.tl);
@@ -1754,7 +1836,7 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
         if (F.fault) {
             R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.segments = 1; R.status = ST_FAULT;
         } else {
-            trace_ray<STATS, TR_FUSED>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, -1, none,
+            trace_ray<STATS, TR_FUSED, SHADOW>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, -1, none,
                                        nullptr, Q, src.pix, L);
         }
         write_pixel(L, src.id, R);
@@ -1846,7 +1928,7 @@ __device__ __forceinline__ int seg_walk_item(const RtLaunch &L, const RtDevScene
     Walker w;
     int end = SEG_SKIP, seat = -1;
     if (valid) {
-        const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
+        const RtCont *rec = lvl_queue(L, L.level - 1) + q;
         const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
         if (j == 0) {
             end = walker_set(S, w, o, d, false, 0, 0, c) < 0 ? SEG_SEATTHROW : SEG_FIN;
@@ -1911,7 +1993,7 @@ __device__ __forceinline__ void seg_first_item(const RtLaunch &L, const RtDevSce
     }
     int2 res = make_int2(-1, -1);
     if (valid && open && cn >= 8 && !fault) {
-        const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
+        const RtCont *rec = lvl_queue(L, L.level - 1) + q;
         const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
         res = scan_first(L, S, o, d, make_raybox(o, d), (uint32_t)stride, (uint32_t)id, cn >> 3, c);
     }
@@ -1964,7 +2046,7 @@ __device__ __forceinline__ void seg_level(const RtLaunch &L, int K)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const bool fault = L.setup->fault != 0;
     const RtFrameSetup F = *L.setup;
-    const RayQueues Q = {L.queue[L.level & 1], lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
+    const RayQueues Q = {lvl_queue(L, L.level), lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
     const SegLane g = seg_lane(L, K);
     const int items = (g.n_rays + g.rpw - 1) / g.rpw;
     for (;;) {
@@ -1982,7 +2064,7 @@ __device__ __forceinline__ void seg_level(const RtLaunch &L, int K)
                 RaySrc src;
                 src.valid = true;
                 src.id = (size_t)q;
-                src.rec = L.queue[(L.level - 1) & 1] + q;
+                src.rec = lvl_queue(L, L.level - 1) + q;
                 src.pix = src.rec->pix;
                 for (int i = 0; i < 3; i++) { src.o[i] = src.rec->o[i]; src.d[i] = src.rec->d[i]; }
                 shade_ray(L, F, Q, src, ocn, out, c);
@@ -2090,7 +2172,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
             if (res != 1 && r < n_rays) {
                 q = r;
                 n = 0;
-                const RtCont *rec = L.queue[(L.level - 1) & 1] + q;
+                const RtCont *rec = lvl_queue(L, L.level - 1) + q;
                 const double o[3] = {rec->o[0], rec->o[1], rec->o[2]}, d[3] = {rec->d[0], rec->d[1], rec->d[2]};
                 rb = make_raybox(o, d);
                 if (walker_set(S, w, o, d, false, 0, 0, c) < 0) L.cand_n[q] = 3;
@@ -2245,7 +2327,7 @@ __global__ void __launch_bounds__(256, MINW) k_first_refill(RtLaunch L)
     const int n_rays = *lvl_ctr(L, L.level - 1);
     int32_t *head = pass_heads(L, L.level, 2);
     const bool fault = L.setup->fault != 0;
-    const RtCont *queue = L.queue[(L.level - 1) & 1];
+    const RtCont *queue = lvl_queue(L, L.level - 1);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     int q = 0, k = 0, n = 0;
     bool busy = false, drained = false;
@@ -2426,7 +2508,7 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
     const int items = n_items(L);
     const RtFrameSetup F = *L.setup;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const RayQueues Q = {L.queue[L.level & 1], lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
+    const RayQueues Q = {lvl_queue(L, L.level), lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
     const int ch = L.claim_chunk;
     const int32_t *ray_cn = seg_mode(L) ? L.ray_cn : L.cand_n;     // segmented levels: k_first's combined status
     const bool queued = RT_EARLY_SHADE && L.level == 0;             // level 0: the rays k_first queued
@@ -2608,8 +2690,9 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     (void)hipGetLastError();                     // a stale error of an earlier runtime call is not ours
     const bool trace = L.rows > 0 && !L.skip_trace;
     // one wave per block (6 per row band of 64), so that the ~100 chain waves of a 1080p frame land
-    // on ~100 CUs: a chain step with its store costs 64 cycles with 4 such waves on a CU against 48
-    // alone (tools/probe/chain_latency.hip)
+    // on ~100 CUs: the CU's vector-memory path is shared by its SIMDs, and a chain step with its
+    // 512-byte store costs 64 cycles with 4 such waves on a CU against 48 alone
+    // (tools/probe/chain_latency.hip)
     hipLaunchKernelGGL(k_frame_start, dim3(1 + 6 * ((std::max(L.rows, 0) + 63) / 64)), dim3(64), 0, st, L.scene, L.cam, L.cfg,
                        L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.row0, L.dirs, trace ? L.ctr : nullptr,
                        L.zero_fault ? L.fault : nullptr,
@@ -2623,7 +2706,11 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     (void)W;
     if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
     // occupancy variants (waves per SIMD the register allocation must admit); RT_OCC selects
-    if (L.counters) {
+    if (L.n_lights > 0) {                        // shadow rays: the fused path (rt_set_lights)
+        if (L.cand) return rt_set_error(RT_E_INVALID, "shadow rays run the fused path only");
+        if (L.counters) launch_persistent(k_trace<true, 2, true>, st, L);
+        else launch_persistent(k_trace<false, 3, true>, st, L);
+    } else if (L.counters) {
         launch_persistent(k_trace<true, 2>, st, L);
     } else if (!L.cand) {
         if (L.occ == 2) launch_persistent(k_trace<false, 2>, st, L);
@@ -2782,7 +2869,8 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *na
         static const std::pair<const void *, const char *> known[] = {
             {(const void *)k_frame_start, "k_frame_start"}, {(const void *)k_trace<true, 2>, "k_trace"},
             {(const void *)k_trace<false, 2>, "k_trace"}, {(const void *)k_trace<false, 3>, "k_trace"},
-            {(const void *)k_trace<false, 4>, "k_trace"}, {(const void *)k_walk_first<4>, "k_walk_first"},
+            {(const void *)k_trace<false, 4>, "k_trace"}, {(const void *)k_trace<true, 2, true>, "k_trace_shadow"},
+            {(const void *)k_trace<false, 3, true>, "k_trace_shadow"}, {(const void *)k_walk_first<4>, "k_walk_first"},
             {(const void *)k_walk_first<4, 64>, "k_walk_first"},
 {(const void *)k_walk<3>, "k_walk"},
             {(const void *)k_walk<4>, "k_walk"}, {(const void *)k_walk<5>, "k_walk"},

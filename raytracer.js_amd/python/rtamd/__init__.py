@@ -218,6 +218,11 @@ class Context:
                     gather={abi.RT_GATHER_NONE: "none", abi.RT_GATHER_RCCL: "rccl",
                             abi.RT_GATHER_PEER: "peer"}[i.gather])
 
+    def set_lights(self, lights, ambient=0.0):
+        """rt_set_lights: shadow rays, a build extension (include/rt.h): [(pos, rgb), ...] point lights,
+        at most abi.RT_MAX_LIGHTS; [] (the default) restores the reference."""
+        _check(self.L.rt_set_lights(self.h, abi.lights_array(lights), len(lights), float(ambient)))
+
     def trace_frame_device(self, cam, cfg, d_rgb_ptr, stream_ptr=None):
         """rt_trace_frame_device: the whole frame into a devices[0] buffer (W*H*3 f32), asynchronous."""
         _check(self.L.rt_trace_frame_device(self.h, C.byref(cam), C.byref(cfg), C.c_void_p(d_rgb_ptr),

@@ -108,6 +108,24 @@ class rt_edit_desc(C.Structure):
                 ("shades", C.c_void_p), ("substance_ri", _P(_d))]
 
 
+RT_MAX_LIGHTS = 4
+
+
+class rt_light(C.Structure):
+    _fields_ = [("pos", _d * 3), ("rgb", _d * 3)]
+
+
+def lights_array(lights):
+    """[(pos, rgb), ...] -> rt_light[RT_MAX_LIGHTS] (shadow rays, rt_set_lights)."""
+    if len(lights) > RT_MAX_LIGHTS:
+        raise ValueError("at most %d lights" % RT_MAX_LIGHTS)
+    arr = (rt_light * RT_MAX_LIGHTS)()
+    for k, (pos, rgb) in enumerate(lights):
+        arr[k].pos[:] = [float(x) for x in pos]
+        arr[k].rgb[:] = [float(x) for x in rgb]
+    return arr
+
+
 class rt_update_stats(C.Structure):
     _fields_ = [("full", _i), ("dirty_nodes", _i), ("new_nodes", _i), ("moved_regions", _i),
                 ("changed_entities", _i), ("pad_", _i), ("bytes", C.c_int64), ("host_ms", _d), ("total_ms", _d)]
@@ -142,7 +160,7 @@ EXPORTS = ("rt_create", "rt_destroy", "rt_last_error", "rt_abi_version", "rt_upl
            "rt_builder_add_many", "rt_builder_desc", "rt_exposure_stats_device", "rt_tonemap_device",
            "rt_tonemap_range", "rt_update_scene", "rt_builder_move", "rt_builder_set_shade",
            "rt_trace_frame_device", "rt_frame_fault", "rt_ctx_info_get", "rt_builder_sync",
-           "rt_debug_rccl_frames", "rt_apply_edit", "rt_scene_node_slots")
+           "rt_debug_rccl_frames", "rt_apply_edit", "rt_scene_node_slots", "rt_set_lights")
 
 # rt_trace_hook: void (*)(int32_t ctx, int32_t device)
 TRACE_HOOK = C.CFUNCTYPE(None, C.c_int32, C.c_int32)
@@ -177,6 +195,7 @@ def declare(lib):
     lib.rt_tonemap_range.argtypes = [_i, P(rt_exposure_stats), _i, _d, _d, _pd]
     lib.rt_update_scene.argtypes = [vp, P(rt_scene_desc), P(rt_update_stats)]
     lib.rt_apply_edit.argtypes = [vp, P(rt_edit_desc), P(rt_update_stats)]
+    lib.rt_set_lights.argtypes = [vp, P(rt_light), _i, _d]
     lib.rt_scene_node_slots.argtypes = [vp, _pi, _i, _pi]
     lib.rt_builder_sync.argtypes = [vp, vp, P(rt_shade), _i, _pd, _i, P(rt_update_stats)]
     lib.rt_builder_move.argtypes = [vp, _i, _pd]

@@ -30,7 +30,7 @@ def test_library_exports_every_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", rtamd.LIB_PATH], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r" T (rt_\w+)$", out, re.M))
     assert set(_declared()) <= exported
-    assert lib.rt_abi_version() == 4
+    assert lib.rt_abi_version() == 5
 
 
 def test_struct_layouts_match_header(tmp_path):

@@ -101,7 +101,7 @@ def test_journal_bounds_itself(tmp_path):
 def test_addon_loads_and_fails_loudly_without_gpu():
     """The addon loads; with no GPU create() throws RT_E_NODEVICE (never a silent CPU path)."""
     js = ("const rt=require(%r);const a=rt.load_addon();"
-          "if(a.abiVersion()!==4)throw Error('abi');"
+          "if(a.abiVersion()!==5)throw Error('abi');"
           "try{a.create(0);console.log('GPU')}catch(e){console.log(e.code)}"
           "try{a.create([0,0],8);console.log('GPU')}catch(e){console.log(e.code)}"
           "try{a.create([]);console.log('empty accepted')}catch(e){console.log(e.code)}") % os.path.join(ROOT, "raytracer.js_amd", "js", "raytracer.js")
