@@ -303,7 +303,7 @@ int  rt_frame_fault(rt_ctx *ctx, int32_t *fault);
 
 /* Shadow rays: a BUILD EXTENSION, off by default (the reference samples no lights,
  * src/raytracer.ts:168-277; BASELINE config 5 names "shadow rays").  Frozen definition (DESIGN.md
- * §3.7; the oracle's orc_set_lights implements the same): with n > 0 point lights, a ray that ends on
+ * §3.6; the oracle's orc_set_lights implements the same): with n > 0 point lights, a ray that ends on
  * a matte surface (REFLECTION, not a mirror, not a light), after alter_ray and the path-length update,
  * at point p with the hit normal nrm and path length `path`, multiplies its colour channel-wise by
  *     s = ambient + sum over lights l (in order) of  rgb_l * (cosine * isl)

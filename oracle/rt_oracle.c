@@ -1212,7 +1212,7 @@ uint32_t orc_scatter_dir(uint64_t seed, uint64_t pixel, uint32_t draws, const do
 double orc_counter_draw_at(uint64_t seed, uint64_t pixel, uint32_t n) { return orc_counter_draw(seed, pixel, n); }
 
 /* ---- shadow rays: a BUILD EXTENSION (the reference samples no lights, src/raytracer.ts:168-277).
- * The frozen definition is include/rt.h's rt_set_lights comment (DESIGN.md §3.7); this is its CPU
+ * The frozen definition is include/rt.h's rt_set_lights comment (DESIGN.md §3.6); this is its CPU
  * statement, the GPU's parity target.  Not pinned by any reference output: parity is against this. */
 int orc_set_lights(oworld *w, const rt_light *lights, int n, double ambient)
 {

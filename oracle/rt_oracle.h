@@ -58,7 +58,7 @@ int      orc_walker_next(owalker *wk, onode **node, onode **pos_tree, int *pos_o
 /* --- scene (src/octree_entity.ts, src/entity.ts, src/entities/) --- */
 int  orc_set_tables(oworld *w, const rt_shade *shades, int n_shades, const double *ri, int n_ri);
 int  orc_set_images(oworld *w, const rt_image_desc *images, int n);      /* ImageTextures (copied) */
-/* shadow rays, a build extension (include/rt.h rt_set_lights; DESIGN.md §3.7): n = 0 is the reference */
+/* shadow rays, a build extension (include/rt.h rt_set_lights; DESIGN.md §3.6): n = 0 is the reference */
 int  orc_set_lights(oworld *w, const rt_light *lights, int n, double ambient);
 double orc_atan(double x);                                                 /* Math.atan (V8 / fdlibm) */
 double orc_atan2(double y, double x);                                      /* Math.atan2 (V8 / fdlibm) */

@@ -1383,7 +1383,7 @@ __device__ __forceinline__ RtCont *lvl_queue(const RtLaunch &L, int k)
     return (k & 1) ? L.queue[1] : L.queue[0];
 }
 
-// ---- shadow rays (a build extension, rt_set_lights; definition: include/rt.h, DESIGN.md §3.7) ----
+// ---- shadow rays (a build extension, rt_set_lights; definition: include/rt.h, DESIGN.md §3.6) ----
 // Whether the shadow ray from q along u (unit) reaches a light at distance dist: its first hit in the
 // reference's walk order decides.  The work is not counted (cs is the caller's scratch).
 __device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, const double q[3], const double u[3], double dist,

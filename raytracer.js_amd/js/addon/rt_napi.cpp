@@ -1,6 +1,6 @@
 // rt_napi.cpp — N-API (v8) binding of librt_amd.so for the JavaScript drop-in (../raytracer.js).
 //
-// Exports create / uploadScene / traceFrame / destroy / lastError / abiVersion.  Typed arrays are
+// Exports create / uploadScene / traceFrame / destroy / lastError / abiVersion (and setLights).  Typed arrays are
 // passed zero-copy (napi_get_typedarray_info) and are only read/written during the call; the call is
 // synchronous and blocks the event loop exactly like the reference's Raytracer.trace_frame()
 // (src/raytracer.ts:308-330).  A negative RT_E_* code becomes a thrown JS Error whose `code` is
@@ -361,6 +361,37 @@ napi_value SceneSlots(napi_env env, napi_callback_info info)
     return o;
 }
 
+// setLights(ctx, [{pos: [x, y, z], rgb: [r, g, b]}, ...], ambient): rt_set_lights, the shadow-ray
+// build extension (include/rt.h); an empty list restores the reference
+napi_value SetLights(napi_env env, napi_callback_info info)
+{
+    size_t argc = 3;
+    napi_value argv[3];
+    NAPI_TRY(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    if (argc < 2) { napi_throw_error(env, "RT_E_INVALID", "setLights(ctx, lights, ambient)"); return nullptr; }
+    rt_ctx *ctx = unwrap(env, argv[0]);
+    if (!ctx) return nullptr;
+    bool is_list = false;
+    NAPI_TRY(napi_is_array(env, argv[1], &is_list));
+    if (!is_list) { napi_throw_error(env, "RT_E_INVALID", "setLights: lights must be an array"); return nullptr; }
+    uint32_t n = 0;
+    NAPI_TRY(napi_get_array_length(env, argv[1], &n));
+    if (n > RT_MAX_LIGHTS) { napi_throw_error(env, "RT_E_INVALID", "setLights: too many lights"); return nullptr; }
+    rt_light lights[RT_MAX_LIGHTS];
+    memset(lights, 0, sizeof lights);
+    for (uint32_t k = 0; k < n; k++) {
+        napi_value e;
+        NAPI_TRY(napi_get_element(env, argv[1], k, &e));
+        if (!get_vec(env, e, "pos", lights[k].pos, 3) || !get_vec(env, e, "rgb", lights[k].rgb, 3)) return nullptr;
+    }
+    double ambient = 0;
+    if (argc >= 3) NAPI_TRY(napi_get_value_double(env, argv[2], &ambient));
+    if (throw_rc(env, rt_set_lights(ctx, lights, (int32_t)n, ambient))) return nullptr;
+    napi_value u;
+    napi_get_undefined(env, &u);
+    return u;
+}
+
 napi_value ApplyEdit(napi_env env, napi_callback_info info)
 {
     size_t argc = 2;
@@ -590,6 +621,7 @@ napi_value Init(napi_env env, napi_value exports)
         {"updateScene", nullptr, UpdateScene, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"applyEdit", nullptr, ApplyEdit, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"sceneSlots", nullptr, SceneSlots, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"setLights", nullptr, SetLights, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"traceFrame", nullptr, TraceFrame, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"lastError", nullptr, LastError, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"abiVersion", nullptr, AbiVersion, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

@@ -43,6 +43,16 @@ export interface RaytracerOptions {
   stats?: boolean;
   /** 'counter': rough mirrors with the counter-based RNG (include/rt.h RT_SCATTER_COUNTER) */
   scatter?: 'counter';
+  /** shadow rays, a build extension the reference lacks (include/rt.h rt_set_lights): at most 4 */
+  lights?: PointLight[];
+  /** the ambient term of the shadow-ray extension (default 0) */
+  ambient?: number;
+}
+
+/** A point light of the shadow-ray extension. */
+export interface PointLight {
+  pos: VectorLike | number[];
+  rgb: VectorLike | number[];
 }
 
 /** Drop-in for the reference `Raytracer`: same constructor and methods; trace_frame() runs on a GPU. */
@@ -58,6 +68,8 @@ export class Raytracer {
   invalidate_scene(): void;
   /** release the GPU context */
   close(): void;
+  /** shadow rays (build extension): lights and ambient for the next frames; [] turns them off */
+  set_lights(lights: PointLight[], ambient?: number): void;
   last_stats: RtStats | null;
   last_hit_entity: Int32Array | null;
   last_hit_node: Int32Array | null;

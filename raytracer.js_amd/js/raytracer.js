@@ -514,7 +514,10 @@ class Raytracer {
 	 * rejected (RT_E_UNSUPPORTED), as scatter_ray's sequential PRNG cannot be reproduced in parallel.
 	 * `options.stats` fills `last_stats` with the frame's work counters (segments, walker steps,
 	 * entity tests); counting runs the slower fused kernel, so without it `last_stats` holds only
-	 * `frame_ms`. */
+	 * `frame_ms`.
+	 * `options.lights` ([{pos, rgb}], pos a vector3 or [x, y, z]) and `options.ambient` turn on shadow
+	 * rays, a BUILD EXTENSION the reference does not have (include/rt.h rt_set_lights, DESIGN.md §3.6);
+	 * `set_lights()` changes them between frames, and no lights (the default) is the reference. */
 	constructor(config, otree, camera, ebuffer, rng, options) {
 		this.camera = camera;
 		this.ebuffer = ebuffer;
@@ -532,6 +535,15 @@ class Raytracer {
 		this.last_hit_entity = null;
 		this.last_hit_node = null;
 		this.last_status = null;
+		this._lights = null;            // shadow rays: sent before the next frame when not null
+		if (this.options.lights) this.set_lights(this.options.lights, this.options.ambient);
+	}
+
+	/** Shadow rays (build extension): point lights [{pos, rgb}] and the ambient term; [] turns them off. */
+	set_lights(lights, ambient) {
+		const vec = (p) => (p && p.v ? p.v : p);
+		this._lights = { list: (lights || []).map((l) => ({ pos: Array.from(vec(l.pos)), rgb: Array.from(vec(l.rgb)) })),
+			ambient: +(ambient || 0) };
 	}
 
 	set_camera(camera) { this.camera = camera; }
@@ -653,6 +665,10 @@ class Raytracer {
 	trace_frame() {
 		const a = load_addon();
 		const scene = this._sync_scene();
+		if (this._lights) {
+			a.setLights(this._ctx, this._lights.list, this._lights.ambient);
+			this._lights = null;
+		}
 		const cam = camera_desc(this.camera);
 		const eb = this.ebuffer;
 		if (eb.width !== cam.width || eb.height !== cam.height) {

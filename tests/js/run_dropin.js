@@ -12,6 +12,7 @@
  *   fields and Sets directly and calls invalidate_scene({ full: true }) (a full re-read, rt_update_scene).
  * --devices: options.devices (one context over several GPUs, or several parts on one GPU).
  * --plain: options {} (no ids, no counters), the default path a host takes; only pixels are written.
+ * --lights JSON: options.lights / options.ambient (shadow rays, a build extension; include/rt.h).
  * --repeat N: after the first frame, N frames timed each with options.stats off, then N with it on
  *   (<out_prefix>.repeat.json).
  */
@@ -66,6 +67,13 @@ const plain = process.argv.includes('--plain');
 const opts = plain ? {} : { keep_ids: true, stats: true };
 if (seed !== null) opts.scatter = 'counter';
 if (di > 0) opts.devices = process.argv[di + 1].split(',').map(Number);
+// --lights JSON: {"lights": [{"pos": [..], "rgb": [..]}], "ambient": a} (shadow rays, a build extension)
+const li = process.argv.indexOf('--lights');
+if (li > 0) {
+	const L = JSON.parse(process.argv[li + 1]);
+	opts.lights = L.lights.map((l) => ({ pos: { v: l.pos }, rgb: l.rgb }));
+	opts.ambient = L.ambient;
+}
 const tracer = new rt.Raytracer(config, world.root, cam, eb, rng, opts);
 const t0 = process.hrtime.bigint();
 tracer.trace_frame();

@@ -181,6 +181,28 @@ def test_dropin_default_options_frame_equals_oracle(tmp_path, name, wh, band_min
     assert "frame_ms" in st and "segments" not in st, st          # no counters: the split passes ran
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("plain", [False, True])
+def test_dropin_shadow_rays_equal_oracle(tmp_path, plain):
+    """options.lights / options.ambient (shadow rays, a build extension: include/rt.h rt_set_lights)
+    through the addon's setLights: the frame equals the oracle's statement of the definition."""
+    spec = scenes.config1_spheres()
+    cam, cfg = scenes.make_camera(160, 120), scenes.make_config(3)
+    lights = [((0.25, 0.75, 0.25), (0.6, 0.5, 0.4)), ((0.5, 0.9, 0.6), (0.2, 0.2, 0.2))]
+    path = _dump(tmp_path, spec, cam, cfg)
+    arg = json.dumps({"lights": [{"pos": list(p), "rgb": list(c)} for p, c in lights], "ambient": 0.15})
+    _node([RUNNER, path, str(tmp_path / "out"), "--lights", arg] + (["--plain"] if plain else []))
+    rgb = np.fromfile(tmp_path / "out.rgb", dtype=np.float32)
+    w, root = oracle.build_scene(spec)
+    w.set_lights(lights, 0.15)
+    ref = w.trace_frame(root, cam, cfg, nthreads=8)
+    assert np.array_equal(rgb.view(np.uint32), ref["rgb"].view(np.uint32))
+    w.set_lights([])
+    assert not np.array_equal(rgb, w.trace_frame(root, cam, cfg, nthreads=8)["rgb"])
+    if not plain:
+        assert np.array_equal(np.fromfile(tmp_path / "out.ent", dtype=np.int32), ref["hit_entity"])
+
+
 EDITS = {
     # scene, moved sphere A, entity B takes C's material, A's new position; the second one creates
     # three octree nodes (add_entity_to_octree extends the tree inward)

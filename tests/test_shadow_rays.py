@@ -1,4 +1,4 @@
-"""Shadow rays: a BUILD EXTENSION (rt_set_lights, include/rt.h; DESIGN.md §3.7).  The reference samples
+"""Shadow rays: a BUILD EXTENSION (rt_set_lights, include/rt.h; DESIGN.md §3.6).  The reference samples
 no lights (src/raytracer.ts:168-277), so no reference output pins this: the oracle's statement of the
 frozen definition (oracle/rt_oracle.c shadow_factor) is the parity target, and the CPU tests below
 check that statement's properties.  Lights off (the default) is the reference bit for bit.
@@ -20,11 +20,6 @@ def _oracle_frame(spec, cam, cfg, lights=None, ambient=0.0):
     if lights is not None:
         w.set_lights(lights, ambient)
     return w.trace_frame(root, cam, cfg, nthreads=8)
-
-
-def _matte_mask(spec, ref):
-    """Pixels whose ray can end on a matte surface (any hit at all: the test compares whole frames)."""
-    return ref["hit_entity"] >= 0
 
 
 def test_oracle_lights_off_is_the_reference():
@@ -66,12 +61,11 @@ def test_oracle_a_light_listed_twice_doubles_its_term():
     assert np.array_equal(two["rgb"][~m3], one["rgb"][~m3])
 
 
-def test_oracle_a_light_inside_an_opaque_box_only_leaves_ambient():
-    """A light enclosed by a matte (non-light) box is blocked from every surface outside it: the
+def test_oracle_a_light_outside_the_room_only_leaves_ambient():
+    """A light outside the room box (matte, not a light) is blocked from every surface inside it: the
     frame equals the dark-light frame of the same ambient."""
     spec = scenes.config1_spheres()
     cam, cfg = scenes.make_camera(48, 32), scenes.make_config(3)
-    # the room box encloses the scene; a light outside it is seen by no surface inside
     outside = [((1.6, 1.7, 1.8), (5.0, 5.0, 5.0))]
     got = _oracle_frame(spec, cam, cfg, outside, 0.25)
     dark = _oracle_frame(spec, cam, cfg, [((1.6, 1.7, 1.8), (0.0, 0.0, 0.0))], 0.25)
