@@ -92,6 +92,21 @@ KERNEL_PASS = {"k_walk": "walk", "k_walk_seg": "walk", "k_walk_refill": "walk", 
                "k_first_seg": "first", "k_first_refill": "first", "k_shade": "shade"}
 TRACE_KERNELS = ("k_walk_first", "k_seg", "k_walk", "k_walk_seg", "k_walk_refill", "k_first", "k_first_seg",
                  "k_first_refill", "k_shade", "k_cont", "k_trace", "k_frame_start")
+# Shadow rays (a build extension, include/rt.h rt_set_lights): --lights K puts the first K of these
+# point lights into every context and the oracle baseline (BASELINE config 5: "4 bounces + shadow
+# rays").  The counted segments exclude the shadow rays (rt_stats does not count them).
+BENCH_LIGHTS = [((0.5, 0.5, 0.95), (0.8, 0.8, 0.8)), ((0.15, 0.85, 0.6), (0.5, 0.4, 0.3)),
+                ((0.85, 0.2, 0.7), (0.3, 0.4, 0.6)), ((0.5, 0.1, 0.3), (0.2, 0.3, 0.2))]
+BENCH_AMBIENT = 0.1
+LIGHTS_ON = []                 # the active list (main sets it from --lights)
+
+
+def with_lights(ctx):
+    if LIGHTS_ON:
+        ctx.set_lights(LIGHTS_ON, BENCH_AMBIENT)
+    return ctx
+
+
 PMC_FRAMES = 4                 # frames the --pmc-child run profiles (after one warm-up frame)
 PMC_PASSES = {
     "fetch": ["FETCH_SIZE"],
@@ -248,6 +263,8 @@ def cpu_baseline_c(spec, cam, cfg, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     w, root = oracle.build_scene(spec)
+    if LIGHTS_ON:
+        w.set_lights(LIGHTS_ON, BENCH_AMBIENT)
     rng = np.random.default_rng(0)
     P = cam.width * cam.height
     order = rng.permutation(P).astype(np.int32)
@@ -319,7 +336,8 @@ def cpu_baseline(spec, scene, cam, cfg, budget_s, deadline, reserve_s=0.0):
     budget_s = max(1.0, min(budget_s, deadline.slice(budget_s * 4, reserve_s) / 4))
     js, js_err = None, None
     try:
-        js = cpu_baseline_js(scene, cam, cfg, budget_s / 2, deadline, reserve_s)
+        # the JS restatement follows the reference, which has no lights
+        js = None if LIGHTS_ON else cpu_baseline_js(scene, cam, cfg, budget_s / 2, deadline, reserve_s)
     except (subprocess.TimeoutExpired, RuntimeError, ValueError, OSError) as e:
         js_err = "%s: %s" % (type(e).__name__, str(e)[-300:])
     c = cpu_baseline_c(spec, cam, cfg, budget_s / 2 if js else budget_s)
@@ -340,7 +358,7 @@ def _kernel_base(name):
 
 def _child_cmd(args):
     return [sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
-            "--stripe", str(args.stripe)]
+            "--stripe", str(args.stripe), "--lights", str(getattr(args, "lights", 0))]
 
 
 def _rocprof(extra, args, timeout_s, keep=None):
@@ -580,6 +598,7 @@ def host_frame_time(ctx, cam, cfg, segments, scene=None, device=0, warm=3, reps=
                     os.environ[k] = v
         try:
             one.upload(scene)
+            with_lights(one)
             ts1, rgb1 = _host_frame_ms(one, cam, cfg, warm, reps)
         finally:
             one.close()
@@ -596,6 +615,8 @@ def js_frame(args, timeout_s):
     tool = os.path.join(ROOT, "tools", "js_frame_time.py")
     if shutil.which("node") is None or not os.path.exists(tool):
         return None
+    if LIGHTS_ON:
+        return dict(error="skipped: --lights (the JS timing tool renders the reference's frame)")
     if timeout_s < 10:
         return dict(error="skipped: %.0f s left of the bench deadline" % timeout_s)
     try:
@@ -617,6 +638,7 @@ def pmc_child(args):
     factory, W, H, refmax = scenes.WORKLOADS[args.config]
     ctx = rtamd.Context(0)
     ctx.upload(rtamd.build_scene(factory()))
+    with_lights(ctx)
     cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
     buf = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda")
     s = torch.cuda.Stream()
@@ -662,7 +684,7 @@ def run_ranks(args, spec, scene, W, H, refmax, world, rank, local):
     for _ in range(P):
         c = rtamd.Context(local)
         c.upload(scene)
-        ctxs.append(c)
+        ctxs.append(with_lights(c))
     ctx = ctxs[0]
     cam, cfg = scenes.make_camera(W, H), scenes.make_config(refmax)
     # explicit streams for librt launches, torch copies and the collectives (the legacy NULL
@@ -738,7 +760,7 @@ def run_devices(args, spec, scene, W, H, refmax, n):
     for _ in range(P):
         c = rtamd.Context(devices=devs, stripe_rows=args.stripe)
         c.upload(scene)
-        ctxs.append(c)
+        ctxs.append(with_lights(c))
     ctx = ctxs[0]
     info = ctx.info()
     if info["n_devices"] != n:
@@ -767,6 +789,7 @@ def run_devices(args, spec, scene, W, H, refmax, n):
     same = all(torch.equal(frames[i].view(torch.int32), frames[0].view(torch.int32)) for i in range(1, P))
     one = rtamd.Context(0)
     one.upload(scene)
+    with_lights(one)
     whole = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
     one.trace_frame_device(cam, cfg, whole.data_ptr(), streams[0].cuda_stream)
     sync()
@@ -832,7 +855,10 @@ def main():
                     help="seconds from start by which the JSON line is printed (phases after the timed frames "
                          "shrink or are skipped to fit; a watchdog prints what exists 30 s after it)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--lights", type=int, default=0, choices=range(len(BENCH_LIGHTS) + 1),
+                    help="shadow rays (build extension): point lights in every frame (0 = the reference)")
     args = ap.parse_args()
+    LIGHTS_ON[:] = BENCH_LIGHTS[:args.lights]
     if args.pmc_child:
         return pmc_child(args)
     deadline = Deadline(args.deadline)
@@ -907,11 +933,14 @@ def report(args, res, spec, scene, W, H, refmax, build_s, deadline, reporter):
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (splitmix64 seed 42 scene, BASELINE.json %s)" % args.config,
-        "config": {"workload": args.config, "scene": spec.name, "width": W, "height": H, "refmax": refmax,
+        "config": {"workload": args.config + ("+%d shadow lights" % len(LIGHTS_ON) if LIGHTS_ON else ""),
+                   "scene": spec.name, "width": W, "height": H, "refmax": refmax,
                    "entities": int(len(spec.entities)), "octree_nodes": int(scene.n_nodes),
                    "segments_per_frame": tot["segments"],
                    "parallelism": "rows%d/stripe%d" % (n_gpus, args.stripe), "mode": res["mode"],
                    "collective": res["collective"], "frames_in_flight": res["P"],
+                   "shadow_lights": [dict(pos=p, rgb=c) for p, c in LIGHTS_ON] if LIGHTS_ON else None,
+                   "shadow_ambient": BENCH_AMBIENT if LIGHTS_ON else None,
                    "frames_identical": res["same"], "counters": tot, "scene_build_s": round(build_s, 3)},
         "roofline": roofline,
         "serial": serial,
