@@ -398,6 +398,49 @@ function camera_dirs(cam) {
 // ---- Ray.trace (src/raytracer.ts:168-277) ----------------------------------------------------------
 const ST_OK = 0, ST_WARN = 1, ST_FAULT = 2;
 
+// ---- shadow rays: a BUILD EXTENSION the reference does not have (include/rt.h rt_set_lights,
+// DESIGN.md §3.6), restated on this object model from the frozen definition: manifest.lights /
+// manifest.ambient.  The C oracle's shadow_factor is the same definition.
+function shadow_blocked(sc, q, u, dist) {
+  const walker = sc.shadow_walker || (sc.shadow_walker = new OctreeWalker(sc.root));
+  try {
+    walker.set_pos_and_dir(q, u);
+    for (;;) {
+      const stop = walker.next();
+      if (stop === undefined) return false;
+      let hit, ent;
+      for (const e of stop.node.value) {
+        const c = e.collision_info({ start: q, dir: u });
+        if (c !== undefined) { hit = c; ent = e; break; }
+      }
+      if (hit === undefined) continue;
+      if (sc.m.shades[ent.shade].light) return false;
+      return vector.length(vector.sub(hit.point, q)) < dist - 1e-3;
+    }
+  } catch (e) {
+    return true;                                     // a throw blocks the light
+  }
+}
+
+function shadow_factor(sc, p, nrm, path_len) {
+  const a = sc.m.ambient, s = [a, a, a];
+  for (const lt of sc.m.lights) {
+    const v = vector.sub(new Vector(lt.pos.slice()), p);
+    const dist = vector.length(v);
+    if (!(dist > 0)) continue;
+    const u = vector.scale(v, 1 / dist);
+    const cosine = vector.dot(nrm, u);
+    if (!(cosine > 0)) continue;
+    const q = vector.add(p, vector.scale(u, 1e-3));
+    if (shadow_blocked(sc, q, u, dist)) continue;
+    const t = (path_len + dist) * sc.m.config.distance_attenuation_factor;
+    const isl = 1.0 / (Number.EPSILON + t ** 2);
+    const k = cosine * isl;
+    for (let c = 0; c < 3; c++) s[c] += lt.rgb[c] * k;
+  }
+  return s;
+}
+
 // `out` holds the colour so far: a throw leaves the ray's colour at that point, as the oracle does
 function trace_ray(sc, walker, start, dir0, start_node, start_sub, out) {
   const { m } = sc, cfg = m.config;
@@ -423,7 +466,13 @@ function trace_ray(sc, walker, start, dir0, start_node, start_sub, out) {
     refpoint = hit.point;
     if (sh.light) { light = true; break; }
     if (sh.response === 0) {                       // REFLECTION
-      if (!sh.mirror) return out;
+      if (!sh.mirror) {
+        if (m.lights && m.lights.length) {          // shadow rays (build extension)
+          const sf = shadow_factor(sc, refpoint, hit.normal, path_len);
+          col = out.rgb = [col[0] * sf[0], col[1] * sf[1], col[2] * sf[2]];
+        }
+        return out;
+      }
       dir = vector.reflection(dir, hit.normal);
       refpoint = vector.add(refpoint, vector.scale(dir, 1e-3));
     } else if (sh.response === 1) {                // TRANSMISSION

@@ -30,7 +30,8 @@ def _vec(v, n):
     return [float(v[i]) for i in range(n)]
 
 
-def export(scene, cam, cfg, pixels, out_dir):
+def export(scene, cam, cfg, pixels, out_dir, lights=(), ambient=0.0):
+    """lights / ambient: shadow rays, a build extension (include/rt.h rt_set_lights)."""
     os.makedirs(out_dir, exist_ok=True)
     arrays = dict(node_pos=(scene.node_pos, "<f8"), node_size=(scene.node_size, "<f8"),
                   node_parent=(scene.node_parent, "<i4"), node_child=(scene.node_child, "<i4"),
@@ -49,7 +50,9 @@ def export(scene, cam, cfg, pixels, out_dir):
         config=dict(refmax=int(cfg.refmax), default_substance=int(cfg.default_substance),
                     sky_rgb=_vec(cfg.sky_rgb, 3), distance_attenuation_factor=float(cfg.distance_attenuation_factor),
                     col_weight=float(cfg.col_weight), sky_image=int(cfg.sky_image)),
-        shades=shades, substance_ri=[float(x) for x in scene.substance_ri])
+        shades=shades, substance_ri=[float(x) for x in scene.substance_ri],
+        lights=[dict(pos=[float(x) for x in p], rgb=[float(x) for x in c]) for p, c in lights],
+        ambient=float(ambient))
     with open(os.path.join(out_dir, "manifest.json"), "w") as f:
         json.dump(man, f)                       # floats as repr: they parse back to the same doubles
 

@@ -48,6 +48,25 @@ def test_js_restatement_equals_oracle(name, W, H, refmax, tmp_path):
     assert (got["segments"] > 1).any()      # bounces are exercised
 
 
+def test_js_restatement_shadow_rays_equal_oracle(tmp_path):
+    """Shadow rays (a build extension): the definition restated on the reference's
+    object model in JavaScript equals the C oracle's statement bit for bit."""
+    spec = scenes.config1_spheres()
+    W, H = 64, 48
+    cam, cfg = scenes.make_camera(W, H), scenes.make_config(3)
+    lights = [((0.25, 0.75, 0.25), (0.6, 0.5, 0.4)), ((0.75, 0.25, 0.75), (0.3, 0.4, 0.9)),
+              ((0.5, 0.9, 0.6), (0.2, 0.2, 0.2))]
+    d = str(tmp_path / "shadow")
+    js_baseline.export(rtamd.build_scene(spec), cam, cfg, np.arange(W * H), d, lights, 0.1)
+    _, got = js_baseline.run(d)
+    w, root = oracle.build_scene(spec)
+    w.set_lights(lights, 0.1)
+    ref = w.trace_frame(root, cam, cfg, nthreads=4)
+    assert np.array_equal(ref["rgb"].reshape(-1, 3).view(np.uint32), got["rgb"].view(np.uint32))
+    w.set_lights([])
+    assert not np.array_equal(ref["rgb"], w.trace_frame(root, cam, cfg, nthreads=4)["rgb"])
+
+
 def test_js_workers_config3_sample(tmp_path):
     """The bench's workload (config 3 scene, 1920x1080) on a pixel sample, split over 3 workers."""
     rng = np.random.default_rng(3)
