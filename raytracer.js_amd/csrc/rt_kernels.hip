@@ -100,6 +100,9 @@ extern __shared__ RtNode s_top[];
 #define RT_BUF_LOADS 0
 #endif
 #if RT_BUF_LOADS
+#ifndef RT_FS_BUFFER
+#define RT_FS_BUFFER 1                          // k_frame_start's row stores: buffer stores (1) / pointers (0)
+#endif
 typedef unsigned int rt_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int rt_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const RtDevScene &S)
@@ -1165,6 +1168,9 @@ __device__ __forceinline__ int wave_min(int v)
 // at most H/2 + W/2 steps of one multiply-add pair, bit-identical to the sequential scan.
 // dirs: SoA planes [3][W*rows], x-major (index x*rows + local row): a wave stores 64 consecutive
 // rows of one column per step, and an 8x8 tile of the walk reads 8 runs of 64 bytes per plane.
+#ifndef RT_FS_BUFFER
+#define RT_FS_BUFFER 1                          // k_frame_start's row stores: buffer stores (1) / pointers (0)
+#endif
 typedef unsigned int rt_u32x2 __attribute__((ext_vector_type(2)));
 #define RT_BUFFER_DWORD3 0x00020000             // gfx9 raw buffer: 32-bit data format, no swizzle
 
@@ -1253,7 +1259,7 @@ __global__ void __launch_bounds__(64) k_frame_start(RtDevScene S, rt_camera_desc
     // address arithmetic in the chain's loop); the plane's size bounds every store.  A plane of
     // 2 GiB or more (over 2^28 pixels in the part) takes 64-bit pointers
     const size_t plane_sz = (size_t)rows * (size_t)W * sizeof(double);
-    if (plane_sz >= ((size_t)1 << 31)) {
+    if (!RT_FS_BUFFER || plane_sz >= ((size_t)1 << 31)) {
         double *p = dirs + (size_t)i * (size_t)rows * (size_t)W + (size_t)from * (size_t)rows + (size_t)lr;
         const ptrdiff_t step = (ptrdiff_t)inc * (ptrdiff_t)rows;
         for (int k = 0; k < n; k++) {

@@ -59,6 +59,27 @@ __global__ void __launch_bounds__(256) k_chain(double *out, long long *cyc, int 
             so += rows * 8;
             rot(x, y, c, s);
         }
+    } else if (V == 7) {                       // wave-uniform base stepped in scalar registers, 32-bit lane offset
+        const char *b0 = reinterpret_cast<const char *>(out) + (size_t)blockIdx.x * blockDim.x * 8;
+        char *b = const_cast<char *>(b0);
+        const unsigned lo = threadIdx.x * 8u;
+#pragma unroll 4
+        for (int k = 0; k < n; k++) {
+            *reinterpret_cast<double *>(b + lo) = x;
+            b += (size_t)rows * 8;
+            rot(x, y, c, s);
+        }
+    } else if (V == 8) {                       // buffer store of a copy taken before the rotation
+        typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+        int so = 0;
+#pragma unroll 4
+        for (int k = 0; k < n; k++) {
+            const double keep = x;
+            rot(x, y, c, s);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, keep), r, t * 8, so, 0);
+            so += rows * 8;
+        }
     } else if (V == 3) {                       // two chains per lane, no stores
 #pragma unroll 4
         for (int k = 0; k < n; k++) { rot(x, y, c, s); rot(x2, y2, c, s); }
@@ -113,6 +134,8 @@ int main()
         run<1>("chain+store", rows, n, out, cyc, 64);
         run<5>("chain+store_pairs", rows, n, out, cyc, 64);
         run<6>("chain+buffer_store", rows, n, out, cyc, 64);
+        run<7>("chain+uniform_base_store", rows, n, out, cyc, 64);
+        run<8>("chain+buffer_store_late", rows, n, out, cyc, 64);
     }
     return 0;
 }
