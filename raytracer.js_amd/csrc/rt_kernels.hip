@@ -1090,6 +1090,9 @@ __device__ __forceinline__ int node_first_hit(const RtDevScene &S, const int4 ne
 #ifndef RT_SCAN_FLAT
 #define RT_SCAN_FLAT 1
 #endif
+#ifndef RT_SCAN_PF
+#define RT_SCAN_PF 0
+#endif
 template <bool FLAT = true>
 __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &S, const double o[3], const double d[3],
                                            const RayBox &rb, uint32_t stride, uint32_t id, int n, Counters &c)
@@ -1111,6 +1114,9 @@ __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &
     // i >= 0: the next record of the current node's hierarchy; slot < prim_end: leaf prims to test
     int k = 0, node = -1, i = -1, slot = 0, prim_end = 0, best_rank = 0x7fffffff, best_slot = -1;
     bool active = n > 0;
+    // RT_SCAN_PF: the next candidate's id is loaded one node ahead, so a node switch waits for the
+    // header load only
+    int nxt = RT_SCAN_PF && n > 0 ? cand_load(L, 0, stride, id) : -1;
     while (active) {
         if (slot < prim_end) {
             const int rk = S.prim[slot].rank;
@@ -1131,7 +1137,13 @@ __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &
         } else if (k >= n) {
             active = false;
         } else {
-            node = cand_load(L, k++, stride, id);
+            if (RT_SCAN_PF) {
+                node = nxt;
+                k++;
+                if (k < n) nxt = cand_load(L, k, stride, id);
+            } else {
+                node = cand_load(L, k++, stride, id);
+            }
             const int4 hdr = ld_node<int4>(S, node, NODE_NENT);
             if (!RT_EMIT_BOX) i = hdr.z;                   // node_first_hit's root_hit: the walk pass
             else if (hdr.x <= S.bvh_leaf) { slot = hdr.y; prim_end = hdr.y + hdr.x; }   // crossed the
