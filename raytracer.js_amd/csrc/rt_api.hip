@@ -667,6 +667,8 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.blend = cfg->col_weight != 1.0;
     if (c->n_lights) {
         if (d.lights_seq != c->lights_seq) {
+            // a frame of this context still in flight may read the old lights: let it finish first
+            if (d.stream) HIP_TRY(hipStreamSynchronize(d.stream));
             if ((r = d.b_lights.ensure(sizeof(rt_light) * RT_MAX_LIGHTS)) != RT_OK) return r;
             HIP_TRY(hipMemcpy(d.b_lights.p, c->lights, sizeof(rt_light) * RT_MAX_LIGHTS, hipMemcpyHostToDevice));
             d.lights_seq = c->lights_seq;
