@@ -238,8 +238,8 @@ def config5(n_tri=1_000_000, n_sph=2000, seed=42):
     Materials ~70% matte / 25% mirror / 5% light; every third small sphere and 8 large ones are GLASS
     with a TRANSMISSION material (refract_ray + entity_at_pos, src/raytracer.ts:135-150,238-249;
     src/octree_entity.ts:191-202).  "Shadow rays" in BASELINE's wording have no counterpart in the
-    reference's Ray.trace (src/raytracer.ts:168-277 never samples lights), so the drop-in does not
-    add them."""
+    reference's Ray.trace (src/raytracer.ts:168-277 never samples lights): they are a build
+    extension, off unless lights are set (rt_set_lights; bench.py --lights K)."""
     st = Stream(seed)
     tri = random_triangles(st, n_tri, 0.0003, max_in_depth=10)
     sph = random_spheres(st, n_sph, 0.002, 0.01, max_in_depth=10)
