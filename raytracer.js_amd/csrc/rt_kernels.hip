@@ -100,12 +100,6 @@ extern __shared__ RtNode s_top[];
 #define RT_BUF_LOADS 0
 #endif
 #if RT_BUF_LOADS
-#ifndef RT_FS_LDS
-#define RT_FS_LDS 0                             // k_frame_start: stores by a second wave through LDS
-#endif
-#ifndef RT_FS_LDS_CH
-#define RT_FS_LDS_CH 32                         // ... horizontal steps per LDS chunk (two chunks in flight)
-#endif
 #ifndef RT_FS_BUFFER
 #define RT_FS_BUFFER 1                          // k_frame_start's row stores: buffer stores (1) / pointers (0)
 #endif
@@ -1097,7 +1091,7 @@ __device__ __forceinline__ int node_first_hit(const RtDevScene &S, const int4 ne
 #define RT_SCAN_FLAT 1
 #endif
 #ifndef RT_SCAN_PF
-#define RT_SCAN_PF 0
+#define RT_SCAN_PF 1                              // next candidate id one node ahead (profiles/r4_v4/ab)
 #endif
 template <bool FLAT = true>
 __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &S, const double o[3], const double d[3],
@@ -1186,12 +1180,6 @@ __device__ __forceinline__ int wave_min(int v)
 // at most H/2 + W/2 steps of one multiply-add pair, bit-identical to the sequential scan.
 // dirs: SoA planes [3][W*rows], x-major (index x*rows + local row): a wave stores 64 consecutive
 // rows of one column per step, and an 8x8 tile of the walk reads 8 runs of 64 bytes per plane.
-#ifndef RT_FS_LDS
-#define RT_FS_LDS 0                             // k_frame_start: stores by a second wave through LDS
-#endif
-#ifndef RT_FS_LDS_CH
-#define RT_FS_LDS_CH 32                         // ... horizontal steps per LDS chunk (two chunks in flight)
-#endif
 #ifndef RT_FS_BUFFER
 #define RT_FS_BUFFER 1                          // k_frame_start's row stores: buffer stores (1) / pointers (0)
 #endif
@@ -1205,7 +1193,7 @@ __device__ __forceinline__ void rotate_1(double &x, double &y, double c, double 
     y = ny;
 }
 
-__global__ void __launch_bounds__(64 * (1 + RT_FS_LDS)) k_frame_start(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
+__global__ void __launch_bounds__(64) k_frame_start(RtDevScene S, rt_camera_desc cam, rt_config_desc cfg,
                                                      RtFrameSetup *setup, int part, int n_parts, int stripe,
                                                      int rows, int row0, double *__restrict__ dirs, int32_t *ctr,
                                                      int32_t *fault, int tl)
@@ -1245,59 +1233,6 @@ __global__ void __launch_bounds__(64 * (1 + RT_FS_LDS)) k_frame_start(RtDevScene
         }
         return;
     }
-#if RT_FS_LDS
-    // RT_FS_LDS: block b >= 1 is two waves over the same 64 rows: wave 0 runs the chains and leaves
-    // each horizontal step's 64 values in LDS (a double-buffered ring of RT_FS_LDS_CH steps), wave 1
-    // stores them, so the chain's wave issues no global stores
-    {
-        __shared__ double ring[2][RT_FS_LDS_CH][64];
-        const int wv = threadIdx.x >> 6;
-        const int wpg = (rows + 63) >> 6;
-        const int hc = (int)(blockIdx.x - 1) / wpg;
-        if (hc >= 6) return;                          // the whole block
-        const int lr0 = ((int)(blockIdx.x - 1) - hc * wpg) << 6, lr = lr0 + lane;
-        const bool valid = lr < rows;
-        const int i = hc >> 1;
-        const bool right = (hc & 1) == 0;
-        const int W = cam.width, H = cam.height;
-        const double c = cam.scan_h[0], sh = right ? cam.scan_h[1] : -cam.scan_h[1];
-        const int from = right ? (W >> 1) : (W >> 1) - 1, inc = right ? 1 : -1;
-        const int n = right ? W - from : from + 1;
-        double f = 0, l = 0;
-        if (wv == 0 && valid) {
-            const int y = row0 + part_row_to_y(lr, part, n_parts, stripe);
-            double u = cam.up[i];
-            f = cam.fr[i];
-            const double cv = cam.scan_v[0];
-            const bool top = y >= (H >> 1);
-            const double sv = top ? cam.scan_v[1] : -cam.scan_v[1];
-            if (!top) rotate_1(f, u, cv, sv);
-            const int steps = top ? y - (H >> 1) : (H >> 1) - 1 - y;
-#pragma unroll 4
-            for (int k = 0; k < steps; k++) rotate_1(f, u, cv, sv);
-            l = cam.lf[i];
-            if (!right) rotate_1(f, l, c, sh);
-        }
-        double *plane = dirs + (size_t)i * (size_t)rows * (size_t)W;
-        const int chunks = (n + RT_FS_LDS_CH - 1) / RT_FS_LDS_CH;
-        for (int chk = 0; chk < chunks; chk++) {
-            double (*buf)[64] = ring[chk & 1];
-            const int k0 = chk * RT_FS_LDS_CH, kn = min(RT_FS_LDS_CH, n - k0);
-            if (wv == 0) {
-#pragma unroll 4
-                for (int j = 0; j < kn; j++) { buf[j][lane] = f; rotate_1(f, l, c, sh); }
-            }
-            __syncthreads();
-            if (wv == 1 && valid) {
-                double *p = plane + (size_t)(from + k0 * inc) * (size_t)rows + (size_t)lr;
-                const ptrdiff_t step = (ptrdiff_t)inc * (ptrdiff_t)rows;
-#pragma unroll 4
-                for (int j = 0; j < kn; j++) { *p = buf[j][lane]; p += step; }
-            }
-        }
-        return;
-    }
-#endif
     // block b >= 1 is one wave: (component, half) is uniform over it and its lanes are 64 consecutive
     // local rows, so the horizontal chain's rotation constants and its store column live in scalar
     // registers and a step's store is one global_store with a scalar base (no per-lane address math)
@@ -2776,7 +2711,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     // on ~100 CUs: the CU's vector-memory path is shared by its SIMDs, and a chain step with its
     // 512-byte store costs 64 cycles with 4 such waves on a CU against 48 alone
     // (tools/probe/chain_latency.hip)
-    hipLaunchKernelGGL(k_frame_start, dim3(1 + 6 * ((std::max(L.rows, 0) + 63) / 64)), dim3(64 * (1 + RT_FS_LDS)), 0, st,
+    hipLaunchKernelGGL(k_frame_start, dim3(1 + 6 * ((std::max(L.rows, 0) + 63) / 64)), dim3(64), 0, st,
                        L.scene, L.cam, L.cfg,
                        L.setup, L.part, L.n_parts, L.stripe_rows, L.rows, L.row0, L.dirs, trace ? L.ctr : nullptr,
                        L.zero_fault ? L.fault : nullptr,
