@@ -82,7 +82,7 @@ struct RtDevice {
     hipStream_t stream = nullptr;
     RtDevScene scene{};
     DevBuf b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters,
-        b_fault, b_lights;
+        b_fault, b_lights, b_shadow;
     uint64_t lights_seq = 0;                     // the rt_set_lights call b_lights holds
     std::vector<std::array<hipEvent_t, 2>> ev;   // trace-kernel timing ring
     int ev_next = 0, ev_count = 0;
@@ -183,7 +183,7 @@ static void release_device(RtDevice &d)
 {
     (void)hipSetDevice(d.device);
     for (DevBuf *b : {&d.b_cand, &d.b_cand_n, &d.b_first, &d.b_queue, &d.b_ctr, &d.b_setup, &d.b_dirs, &d.b_rgb,
-                      &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault, &d.b_lights})
+                      &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault, &d.b_lights, &d.b_shadow})
         b->release();
     for (auto &e : d.ev)
         for (hipEvent_t x : e)
@@ -677,7 +677,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
         L.ambient = c->ambient;
         L.lights = (const rt_light *)d.b_lights.p;
     }
-    if (c->split && !c->n_lights && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {
+    if (c->split && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot
         // be allocated the frame runs the fused kernel instead (same results).
         // the walk kernels address the lists with 32-bit byte offsets (cand_store): cand_cap * P * 4 < 2^32
@@ -692,6 +692,17 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
             L.queue[0] = (RtCont *)d.b_queue.p;
             L.queue[1] = L.queue[0] + P;
             L.ovf = L.queue[1] + P;
+            // shadow rays: matte ends are deferred to k_shadow (at most one per ray)
+            if (c->n_lights) {
+                if (d.b_shadow.ensure(sizeof(RtShadowRec) * (size_t)P) == RT_OK) {
+                    L.shadow_q = (RtShadowRec *)d.b_shadow.p;
+                } else {
+                    (void)hipGetLastError();
+                    L.cand = nullptr;                   // the fused kernel runs the frame
+                    L.cand_n = nullptr;
+                    L.first = nullptr;
+                }
+            }
         } else {
             (void)hipGetLastError();
             L.cand = nullptr;

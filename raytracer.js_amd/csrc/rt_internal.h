@@ -114,6 +114,15 @@ struct RtLate {
 };
 static_assert(sizeof(RtLate) == 32, "RtLate must stay 32 bytes");
 
+// Shadow rays on the split path (rt_set_lights): a ray that ended on a matte surface, deferred to
+// k_shadow with what its light factor needs (hit point, normal, colour, path length) and what
+// write_pixel writes.
+struct RtShadowRec {
+    double p[3], n[3], col[3], path;
+    int32_t pix, hit_ent, hit_node, segments;
+};
+static_assert(sizeof(RtShadowRec) == 96, "RtShadowRec must stay 96 bytes");
+
 // Per-frame state computed on the device by the setup kernel.
 struct RtFrameSetup {
     int32_t start_tree;   // node_at_pos(otree, camera.pos) → tree (-1: null)
@@ -242,6 +251,8 @@ struct RtLaunch {
     int32_t n_lights;
     double ambient;
     const rt_light *lights;
+    RtShadowRec *shadow_q;                      // split path with lights: [rows*W] deferred matte ends
+                                                // (count ctr[2], claim head ctr[3]), else null
 };
 
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };

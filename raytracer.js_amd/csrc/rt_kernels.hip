@@ -1456,6 +1456,22 @@ __device__ __forceinline__ void shadow_factor(const RtDevScene &S, const RtLaunc
     }
 }
 
+// Split path with lights: the matte end of a ray, deferred to k_shadow (count L.ctr[2]).
+__device__ __forceinline__ void shadow_push(const RtLaunch &L, const double p[3], const double n[3], double col0,
+                                            double col1, double col2, double path, const RayResult &R, int pix)
+{
+    const int k = wave_reserve(L.ctr + 2);
+    RtShadowRec &e = L.shadow_q[k];
+    e.p[0] = p[0]; e.p[1] = p[1]; e.p[2] = p[2];
+    e.n[0] = n[0]; e.n[1] = n[1]; e.n[2] = n[2];
+    e.col[0] = col0; e.col[1] = col1; e.col[2] = col2;
+    e.path = path;
+    e.pix = pix;
+    e.hit_ent = R.hit_ent;
+    e.hit_node = R.hit_node;
+    e.segments = R.segments;
+}
+
 template <bool SHADOW> struct MatteHit {
     bool on = false;
     double n[3];
@@ -1472,7 +1488,9 @@ template <> struct MatteHit<false> {};
 // walker re-seat of src/raytracer.ts:254 is still to do).
 enum { TR_FUSED = 0, TR_LIST = 1 };
 
-template <bool STATS, int MODE, bool SHADOW = false>
+// SHADOW: shadow rays inline (the fused kernel with lights); DEFER: a matte end is deferred to
+// k_shadow when the split path has lights (L.shadow_q) — the passes of the split path, not k_trace
+template <bool STATS, int MODE, bool SHADOW = false, bool DEFER = true>
 __device__ __forceinline__ void trace_ray(const RtDevScene &S, const RtFrameSetup &F, const rt_config_desc &cfg, bool cull,
                           int diag, const double cam_pos[3], const double dir0[3], RayResult &R, Counters &c,
                           int cn, const ListHit &pre, const RtCont *rs, const RayQueues &Q, int pix,
@@ -1588,6 +1606,10 @@ __device__ __forceinline__ void trace_ray(const RtDevScene &S, const RtFrameSetu
                 if constexpr (SHADOW) {                         // shadow rays after the walk (below)
                     matte.on = true;
                     matte.n[0] = h.n[0]; matte.n[1] = h.n[1]; matte.n[2] = h.n[2];
+                } else if (DEFER && L.shadow_q) {               // split path: k_shadow finishes it
+                    shadow_push(L, o, h.n, col0, col1, col2, path, R, pix);
+                    R.status = ST_DEFER;
+                    return;
                 }
                 goto done;
             }
@@ -1854,7 +1876,7 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
         if (F.fault) {
             R.rgb[0] = R.rgb[1] = R.rgb[2] = 0; R.hit_ent = R.hit_node = -1; R.segments = 1; R.status = ST_FAULT;
         } else {
-            trace_ray<STATS, TR_FUSED, SHADOW>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, -1, none,
+            trace_ray<STATS, TR_FUSED, SHADOW, false>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, src.d, R, c, -1, none,
                                        nullptr, Q, src.pix, L);
         }
         write_pixel(L, src.id, R);
@@ -2418,7 +2440,9 @@ __device__ __forceinline__ void first_finish(const RtLaunch &L, const RaySrc &sr
         // level 0: end the plain terminal rays here; queue the rest for k_shade (ray_cn is free at
         // level 0), wave by wave so a shading wave keeps a tile's rays together
         RayResult R;
-        if (!(cn >= 0 && !fault && early_shade(L, src, cn, res, R))) L.ray_cn[wave_reserve(shade_n(L))] = (int)src.id;
+        // (with lights a matte end is deferred to k_shadow: every ray goes to k_shade)
+        if (!(cn >= 0 && !fault && !L.shadow_q && early_shade(L, src, cn, res, R)))
+            L.ray_cn[wave_reserve(shade_n(L))] = (int)src.id;
         else write_pixel(L, (size_t)src.pix, R);
     }
     reinterpret_cast<int2 *>(L.first)[src.id] = res;
@@ -2577,7 +2601,35 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
         RayResult R;
         trace_ray<false, TR_FUSED>(L.scene, F, L.cfg, L.cull != 0, L.diag, L.cam.pos, e->d, R, c, -1, none, e, Q,
                                    e->pix, L);
-        write_pixel(L, (size_t)e->pix, R);
+        if (R.status != ST_DEFER) write_pixel(L, (size_t)e->pix, R);     // ST_DEFER: k_shadow writes it
+    }
+}
+
+// Shadow rays on the split path (rt_set_lights): the matte ends the frame's passes
+// deferred (L.shadow_q, count ctr[2]), one lane each: the light factor (the fused kernel's
+// shadow_factor, same operations), then the pixel.  Runs after k_cont.
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_shadow(RtLaunch L)
+{
+    TL_SCOPE(L.tl);
+    const int lane = threadIdx.x & 63;
+    const int n = L.ctr[2];
+    const bool cull = L.cull != 0;
+    for (;;) {
+        const int base = claim(L.ctr + 3, lane) * 64;
+        if (base >= n) break;
+        const int q = base + lane;
+        if (q >= n) continue;
+        const RtShadowRec e = L.shadow_q[q];
+        double sf[3];
+        shadow_factor(L.scene, L, cull, e.p, e.n, e.path, sf);
+        RayResult R;
+        R.rgb[0] = e.col[0] * sf[0]; R.rgb[1] = e.col[1] * sf[1]; R.rgb[2] = e.col[2] * sf[2];
+        R.hit_ent = e.hit_ent;
+        R.hit_node = e.hit_node;
+        R.segments = e.segments;
+        R.status = ST_OK;
+        write_pixel(L, (size_t)e.pix, R);
     }
 }
 
@@ -2725,12 +2777,13 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     (void)W;
     if (ev_begin) HIP_TRY(hipEventRecord((hipEvent_t)ev_begin, st));
     // occupancy variants (waves per SIMD the register allocation must admit); RT_OCC selects
-    if (L.n_lights > 0) {                        // shadow rays: the fused path (rt_set_lights)
-        if (L.cand) return rt_set_error(RT_E_INVALID, "shadow rays run the fused path only");
-        if (L.counters) launch_persistent(k_trace<true, 2, true>, st, L);
-        else launch_persistent(k_trace<false, 3, true>, st, L);
-    } else if (L.counters) {
-        launch_persistent(k_trace<true, 2>, st, L);
+    // shadow rays (rt_set_lights): the fused kernels run them inline, the split path defers the
+    // matte ends to k_shadow
+    if (L.counters) {
+        if (L.n_lights > 0) launch_persistent(k_trace<true, 2, true>, st, L);
+        else launch_persistent(k_trace<true, 2>, st, L);
+    } else if (L.n_lights > 0 && !L.cand) {
+        launch_persistent(k_trace<false, 3, true>, st, L);
     } else if (!L.cand) {
         if (L.occ == 2) launch_persistent(k_trace<false, 2>, st, L);
         else if (L.occ == 4) launch_persistent(k_trace<false, 4>, st, L);
@@ -2845,6 +2898,8 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
         Lc.late_write = 1;
         launch_persistent(k_cont<3>, st, Lc,
                           cont_hint == 0 && RT_NO_OP_BLOCKS > 0 && L.lv_blocks <= 0 ? RT_NO_OP_BLOCKS : level_blocks(L, cont_hint));
+        // shadow rays (rt_set_lights): the deferred matte ends, after every pass that defers them
+        if (L.shadow_q) launch_persistent(k_shadow<3>, st, Lc);
         // this frame's counters come back for the next frames' grid hints (any recent frame will do)
         if (L.ctr_out) {
             HIP_TRY(hipMemcpyAsync(L.ctr_out, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
@@ -2899,7 +2954,7 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *na
             {(const void *)k_first<4>, "k_first"}, {(const void *)k_first<6>, "k_first"}, {(const void *)k_first<8>, "k_first"},
             {(const void *)k_first_refill<6>, "k_first_refill"}, {(const void *)k_first_seg<4>, "k_first_seg"},
             {(const void *)k_shade<3>, "k_shade"}, {(const void *)k_shade<4>, "k_shade"}, {(const void *)k_shade<5>, "k_shade"},
-            {(const void *)k_cont<3>, "k_cont"}};
+            {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<3>, "k_shadow"}};
         for (int i = 0; i < n; i++) {
             for (int q = 0; q < 4; q++) rec4[4 * i + q] = v[4 * i + q];
             const char *nm = "?";

@@ -92,18 +92,27 @@ def test_light_arrays_bounded():
 
 # ---- GPU parity against the oracle's statement ----------------------------------------------------
 
+SPLIT = {"RT_FUSE_MAX": "0", "RT_FUSE_LIST": "0"}      # every frame on the split path (k_shadow)
+
 SHADOW_CASES = [
+    # config 1 (few entities: the fused kernel, shadow rays inline) and forced onto the split path
     ("config1", (160, 120), 3, LIGHTS, 0.1, {}),
+    ("config1", (160, 120), 3, LIGHTS, 0.1, {"env": SPLIT}),
+    # small4: the split path, matte ends deferred to k_shadow from k_shade and the segmented levels
     ("small4", (128, 96), 4, LIGHTS[1:], 0.0, {}),
-    ("small4", (128, 96), 4, LIGHTS, 0.3, {"stats": True}),
+    ("small4", (128, 96), 4, LIGHTS, 0.3, {"stats": True}),                 # the fused counting kernel
     ("small4", (96, 64), 3, LIGHTS[:2], 0.2, {"devices": [0, 0]}),
+    ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": dict(SPLIT, RT_CAND_CAP="2")}),   # overflow: k_cont defers
+    ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": dict(SPLIT, RT_SEG="1")}),        # unsegmented levels
     ("config1", (96, 64), 3, LIGHTS, 0.0, {"blend": 0.25}),
 ]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,wh,refmax,lights,ambient,opt", SHADOW_CASES)
-def test_shadow_rays_equal_oracle(name, wh, refmax, lights, ambient, opt):
+def test_shadow_rays_equal_oracle(monkeypatch, name, wh, refmax, lights, ambient, opt):
+    for k, v in opt.get("env", {}).items():
+        monkeypatch.setenv(k, v)                      # read at rt_create
     spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4)}[name]()
     cam = scenes.make_camera(*wh)
     blend = opt.get("blend")
