@@ -316,8 +316,8 @@ int  rt_frame_fault(rt_ctx *ctx, int32_t *fault);
  * t = (path + dist) * distance_attenuation_factor and isl = 1/(EPSILON + t*t) (the reference's
  * inverse-square law, src/raytracer.ts:274-275).  Shadow-ray tests are not counted in rt_stats, and
  * hit ids / status stay those of the primary ray.  n = 0 (the default) restores the reference's
- * behaviour bit for bit.  Frames with lights run the fused one-kernel path.  Applies to the
- * context's later frames; not while a frame of the context is in flight. */
+ * behaviour bit for bit.  Applies to the context's later frames (a changed list waits for the
+ * context's frame in flight). */
 #define RT_MAX_LIGHTS 4
 typedef struct rt_light {
     double pos[3];
