@@ -2608,6 +2608,9 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
 // Shadow rays on the split path (rt_set_lights): the matte ends the frame's passes
 // deferred (L.shadow_q, count ctr[2]), one lane each: the light factor (the fused kernel's
 // shadow_factor, same operations), then the pixel.  Runs after k_cont.
+#ifndef RT_SHADOW_OCC
+#define RT_SHADOW_OCC 3                          // waves per SIMD k_shadow's registers must admit
+#endif
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_shadow(RtLaunch L)
 {
@@ -2899,7 +2902,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
         launch_persistent(k_cont<3>, st, Lc,
                           cont_hint == 0 && RT_NO_OP_BLOCKS > 0 && L.lv_blocks <= 0 ? RT_NO_OP_BLOCKS : level_blocks(L, cont_hint));
         // shadow rays (rt_set_lights): the deferred matte ends, after every pass that defers them
-        if (L.shadow_q) launch_persistent(k_shadow<3>, st, Lc);
+        if (L.shadow_q) launch_persistent(k_shadow<RT_SHADOW_OCC>, st, Lc);
         // this frame's counters come back for the next frames' grid hints (any recent frame will do)
         if (L.ctr_out) {
             HIP_TRY(hipMemcpyAsync(L.ctr_out, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
@@ -2954,7 +2957,7 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *na
             {(const void *)k_first<4>, "k_first"}, {(const void *)k_first<6>, "k_first"}, {(const void *)k_first<8>, "k_first"},
             {(const void *)k_first_refill<6>, "k_first_refill"}, {(const void *)k_first_seg<4>, "k_first_seg"},
             {(const void *)k_shade<3>, "k_shade"}, {(const void *)k_shade<4>, "k_shade"}, {(const void *)k_shade<5>, "k_shade"},
-            {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<3>, "k_shadow"}};
+            {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<RT_SHADOW_OCC>, "k_shadow"}};
         for (int i = 0; i < n; i++) {
             for (int q = 0; q < 4; q++) rec4[4 * i + q] = v[4 * i + q];
             const char *nm = "?";
