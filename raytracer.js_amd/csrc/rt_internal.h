@@ -119,9 +119,10 @@ static_assert(sizeof(RtLate) == 32, "RtLate must stay 32 bytes");
 // write_pixel writes.
 struct RtShadowRec {
     double p[3], n[3], col[3], path;
+    double s[3];                                // the light factor so far (ambient, then light by light)
     int32_t pix, hit_ent, hit_node, segments;
 };
-static_assert(sizeof(RtShadowRec) == 96, "RtShadowRec must stay 96 bytes");
+static_assert(sizeof(RtShadowRec) == 120, "RtShadowRec must stay 120 bytes");
 
 // Per-frame state computed on the device by the setup kernel.
 struct RtFrameSetup {
@@ -253,9 +254,14 @@ struct RtLaunch {
     const rt_light *lights;
     RtShadowRec *shadow_q;                      // split path with lights: [rows*W] deferred matte ends
                                                 // (count ctr[2], claim head ctr[3]), else null
+    int32_t shadow_light;                       // the light of a k_shadow_walk / k_shadow_first launch
 };
 
-enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };
+// ctr: [0] overflow count, [1] its claim head, [2] deferred matte ends (shadow rays), [3] their
+// write pass's head; a block of RT_CTR_LEVEL per bounce level from 4; then the shadow passes' claim
+// heads (walk and first-hit per light)
+enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_SHADOW = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1),
+       RT_CTR_INTS = RT_CTR_SHADOW + 16 };
 
 // walk_wait / walk_done (host-frame bands): the level-0 walk pass waits for event walk_wait (the
 // previous band's level-0 walk) and walk_done is recorded after it, so bands' walks run in order.

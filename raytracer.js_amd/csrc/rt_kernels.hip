@@ -1430,29 +1430,47 @@ __device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, c
     }
 }
 
-// The matte hit's light factor s (per channel): ambient + the unblocked lights' rgb * cosine * isl.
+// The shadow ray of a matte hit (point p, normal nrm) toward light lt: false when the light is
+// skipped (dist or cosine not > 0); else its start q, direction u, distance and cosine.
+__device__ __forceinline__ bool shadow_ray(const rt_light &lt, const double p[3], const double nrm[3], double q[3],
+                                           double u[3], double &dist, double &cosine)
+{
+    const double v0 = lt.pos[0] - p[0], v1 = lt.pos[1] - p[1], v2 = lt.pos[2] - p[2];
+    dist = sqrt(dot3(v0, v1, v2, v0, v1, v2));
+    if (!(dist > 0)) return false;
+    const double inv = 1.0 / dist;
+    u[0] = v0 * inv; u[1] = v1 * inv; u[2] = v2 * inv;
+    cosine = dot3(nrm[0], nrm[1], nrm[2], u[0], u[1], u[2]);
+    if (!(cosine > 0)) return false;
+    q[0] = p[0] + u[0] * 1e-3; q[1] = p[1] + u[1] * 1e-3; q[2] = p[2] + u[2] * 1e-3;
+    return true;
+}
+
+// An unblocked light's term, added to s: rgb * (cosine * isl), isl of the whole path length.
+__device__ __forceinline__ void shadow_add(const RtLaunch &L, const rt_light &lt, double path, double dist,
+                                           double cosine, double s[3])
+{
+    const double t = (path + dist) * L.cfg.distance_attenuation_factor;
+    const double isl = 1.0 / (2.220446049250313e-16 + t * t);
+    const double k = cosine * isl;
+    s[0] += lt.rgb[0] * k;
+    s[1] += lt.rgb[1] * k;
+    s[2] += lt.rgb[2] * k;
+}
+
+// The matte hit's light factor s (per channel): ambient + the unblocked lights' rgb * cosine * isl
+// (the fused kernels; the split path runs the same steps as k_shadow_walk / k_shadow_first passes).
 __device__ __forceinline__ void shadow_factor(const RtDevScene &S, const RtLaunch &L, bool cull, const double p[3],
-                              const double nrm[3], double path, double s[3])
+                                              const double nrm[3], double path, double s[3])
 {
     Counters cs = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     s[0] = s[1] = s[2] = L.ambient;
     for (int l = 0; l < L.n_lights; l++) {
         const rt_light lt = L.lights[l];
-        const double v0 = lt.pos[0] - p[0], v1 = lt.pos[1] - p[1], v2 = lt.pos[2] - p[2];
-        const double dist = sqrt(dot3(v0, v1, v2, v0, v1, v2));
-        if (!(dist > 0)) continue;
-        const double inv = 1.0 / dist;
-        const double u[3] = {v0 * inv, v1 * inv, v2 * inv};
-        const double cosine = dot3(nrm[0], nrm[1], nrm[2], u[0], u[1], u[2]);
-        if (!(cosine > 0)) continue;
-        const double q[3] = {p[0] + u[0] * 1e-3, p[1] + u[1] * 1e-3, p[2] + u[2] * 1e-3};
+        double q[3], u[3], dist, cosine;
+        if (!shadow_ray(lt, p, nrm, q, u, dist, cosine)) continue;
         if (shadow_blocked(S, cull, q, u, dist, cs)) continue;
-        const double t = (path + dist) * L.cfg.distance_attenuation_factor;
-        const double isl = 1.0 / (2.220446049250313e-16 + t * t);
-        const double k = cosine * isl;
-        s[0] += lt.rgb[0] * k;
-        s[1] += lt.rgb[1] * k;
-        s[2] += lt.rgb[2] * k;
+        shadow_add(L, lt, path, dist, cosine, s);
     }
 }
 
@@ -1466,6 +1484,7 @@ __device__ __forceinline__ void shadow_push(const RtLaunch &L, const double p[3]
     e.n[0] = n[0]; e.n[1] = n[1]; e.n[2] = n[2];
     e.col[0] = col0; e.col[1] = col1; e.col[2] = col2;
     e.path = path;
+    e.s[0] = e.s[1] = e.s[2] = L.ambient;
     e.pix = pix;
     e.hit_ent = R.hit_ent;
     e.hit_node = R.hit_node;
@@ -2606,28 +2625,109 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
 }
 
 // Shadow rays on the split path (rt_set_lights): the matte ends the frame's passes
-// deferred (L.shadow_q, count ctr[2]), one lane each: the light factor (the fused kernel's
-// shadow_factor, same operations), then the pixel.  Runs after k_cont.
-#ifndef RT_SHADOW_OCC
-#define RT_SHADOW_OCC 3                          // waves per SIMD k_shadow's registers must admit
-#endif
+// deferred (L.shadow_q, count ctr[2]) get their light factor as a walk pass and a first-hit pass per
+// light, the split path's own machinery (walk_item: the candidate lists of the shadow ray, seated
+// like a continuation; scan_first: the first candidate with an exact hit), then k_shadow writes the
+// pixels.  The first hit decides as shadow_blocked does: a hit found in the list decides by its
+// distance (or, on a light, lets the light through); no hit blocks only after a throw or the step
+// cap (cand_n's end status); an overflowed list runs shadow_blocked itself.  Record q's lists use
+// slot q of the frame's candidate buffers, free once k_cont is done.
+constexpr int32_t SHADOW_NO_RAY = -2;             // cand_n: this light is skipped for the record
+
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_shadow_walk(RtLaunch L)
+{
+    TL_SCOPE(L.tl);
+    const int lane = threadIdx.x & 63;
+    const int n = L.ctr[2];
+    const RtFrameSetup F = *L.setup;
+    const RtDevScene &S = L.scene;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    const rt_light lt = L.lights[L.shadow_light];
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    stage_top(S);
+    for (;;) {
+        const int base = claim(L.ctr + RT_CTR_SHADOW + 2 * L.shadow_light, lane) * 64;
+        if (base >= n) break;
+        const int q = base + lane;
+        if (q >= n) continue;
+        const RtShadowRec &e = L.shadow_q[q];
+        RaySrc src;
+        double dist, cosine;
+        if (!shadow_ray(lt, e.p, e.n, src.o, src.d, dist, cosine)) {
+            L.cand_n[q] = SHADOW_NO_RAY;
+            continue;
+        }
+        src.valid = true;
+        src.id = (size_t)q;
+        src.pix = e.pix;
+        src.rec = L.ovf;                          // non-null: seated like a continuation
+        walk_item(L, S, F, src, stride, c);
+    }
+}
+
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_shadow_first(RtLaunch L)
+{
+    TL_SCOPE(L.tl);
+    const int lane = threadIdx.x & 63;
+    const int n = L.ctr[2];
+    const RtDevScene &S = L.scene;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    const bool cull = L.cull != 0;
+    const rt_light lt = L.lights[L.shadow_light];
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (;;) {
+        const int base = claim(L.ctr + RT_CTR_SHADOW + 2 * L.shadow_light + 1, lane) * 64;
+        if (base >= n) break;
+        const int q = base + lane;
+        if (q >= n) continue;
+        const int cn = L.cand_n[q];
+        if (cn == SHADOW_NO_RAY) continue;
+        RtShadowRec &e = L.shadow_q[q];
+        double o[3], d[3], dist, cosine;
+        shadow_ray(lt, e.p, e.n, o, d, dist, cosine);
+        bool blocked;
+        if (cn < 0) {                                 // the list overflowed: the walk itself
+            blocked = shadow_blocked(S, cull, o, d, dist, c);
+        } else {
+            const int2 res = scan_first<true>(L, S, o, d, make_raybox(o, d), (uint32_t)stride, (uint32_t)q, cn >> 2, c);
+            if (res.y < 0) {
+                blocked = (cn & 3) != 0;              // the walk threw or reached the step cap
+            } else {
+                const RtPrim &pr = S.prim[res.y];
+                Hit h;
+                if (prim_hit(pr, o, d, h) < 0) blocked = true;              // the winner throws
+                else if (S.shades[pr.meta >> 2].light) blocked = false;
+                else {
+                    const double a = h.p[0] - o[0], b = h.p[1] - o[1], f = h.p[2] - o[2];
+                    blocked = sqrt(dot3(a, b, f, a, b, f)) < dist - 1e-3;
+                }
+            }
+        }
+        if (!blocked) {
+            double s3[3] = {e.s[0], e.s[1], e.s[2]};
+            shadow_add(L, lt, e.path, dist, cosine, s3);
+            e.s[0] = s3[0]; e.s[1] = s3[1]; e.s[2] = s3[2];
+        }
+    }
+}
+
+// The deferred matte ends' pixels: colour times the light factor.  Runs after the lights' passes.
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_shadow(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
     const int n = L.ctr[2];
-    const bool cull = L.cull != 0;
     for (;;) {
         const int base = claim(L.ctr + 3, lane) * 64;
         if (base >= n) break;
         const int q = base + lane;
         if (q >= n) continue;
         const RtShadowRec e = L.shadow_q[q];
-        double sf[3];
-        shadow_factor(L.scene, L, cull, e.p, e.n, e.path, sf);
         RayResult R;
-        R.rgb[0] = e.col[0] * sf[0]; R.rgb[1] = e.col[1] * sf[1]; R.rgb[2] = e.col[2] * sf[2];
+        R.rgb[0] = e.col[0] * e.s[0]; R.rgb[1] = e.col[1] * e.s[1]; R.rgb[2] = e.col[2] * e.s[2];
         R.hit_ent = e.hit_ent;
         R.hit_node = e.hit_node;
         R.segments = e.segments;
@@ -2902,7 +3002,15 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
         launch_persistent(k_cont<3>, st, Lc,
                           cont_hint == 0 && RT_NO_OP_BLOCKS > 0 && L.lv_blocks <= 0 ? RT_NO_OP_BLOCKS : level_blocks(L, cont_hint));
         // shadow rays (rt_set_lights): the deferred matte ends, after every pass that defers them
-        if (L.shadow_q) launch_persistent(k_shadow<RT_SHADOW_OCC>, st, Lc);
+        if (L.shadow_q) {
+            for (int l = 0; l < L.n_lights; l++) {
+                RtLaunch Ls = Lc;
+                Ls.shadow_light = l;
+                launch_persistent(k_shadow_walk<4>, st, Ls);
+                launch_persistent(k_shadow_first<4>, st, Ls);
+            }
+            launch_persistent(k_shadow<8>, st, Lc);
+        }
         // this frame's counters come back for the next frames' grid hints (any recent frame will do)
         if (L.ctr_out) {
             HIP_TRY(hipMemcpyAsync(L.ctr_out, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
@@ -2957,7 +3065,8 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *na
             {(const void *)k_first<4>, "k_first"}, {(const void *)k_first<6>, "k_first"}, {(const void *)k_first<8>, "k_first"},
             {(const void *)k_first_refill<6>, "k_first_refill"}, {(const void *)k_first_seg<4>, "k_first_seg"},
             {(const void *)k_shade<3>, "k_shade"}, {(const void *)k_shade<4>, "k_shade"}, {(const void *)k_shade<5>, "k_shade"},
-            {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<RT_SHADOW_OCC>, "k_shadow"}};
+            {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<8>, "k_shadow"},
+            {(const void *)k_shadow_walk<4>, "k_shadow_walk"}, {(const void *)k_shadow_first<4>, "k_shadow_first"}};
         for (int i = 0; i < n; i++) {
             for (int q = 0; q < 4; q++) rec4[4 * i + q] = v[4 * i + q];
             const char *nm = "?";
