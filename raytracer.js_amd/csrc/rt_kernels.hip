@@ -1117,10 +1117,6 @@ __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &
     // RT_SCAN_PF: the next candidate's id is loaded one node ahead, so a node switch waits for the
     // header load only
     int nxt = RT_SCAN_PF && n > 0 ? cand_load(L, 0, stride, id) : -1;
-    // RT_SCAN_PF >= 2: the next candidate's header too, loaded at the end of the trip after a node
-    // switch (when its id has had a trip to arrive), so a switch waits for no load at all
-    int4 nh = make_int4(0, 0, 0, 0);
-    int nh_state = 0;                                  // 0 none, 1 id just loaded, 2 header loaded
     while (active) {
         if (slot < prim_end) {
             const int rk = S.prim[slot].rank;
@@ -1141,25 +1137,17 @@ __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &
         } else if (k >= n) {
             active = false;
         } else {
-            int4 hdr;
             if (RT_SCAN_PF) {
                 node = nxt;
-                hdr = RT_SCAN_PF >= 2 && nh_state == 2 ? nh : ld_node<int4>(S, node, NODE_NENT);
                 k++;
                 if (k < n) nxt = cand_load(L, k, stride, id);
-                nh_state = 1;
             } else {
                 node = cand_load(L, k++, stride, id);
-                hdr = ld_node<int4>(S, node, NODE_NENT);
             }
+            const int4 hdr = ld_node<int4>(S, node, NODE_NENT);
             if (!RT_EMIT_BOX) i = hdr.z;                   // node_first_hit's root_hit: the walk pass
             else if (hdr.x <= S.bvh_leaf) { slot = hdr.y; prim_end = hdr.y + hdr.x; }   // crossed the
             else i = hdr.z + 1;                            // root box: a leaf root's prims, or its children
-            continue;
-        }
-        if (RT_SCAN_PF >= 2 && nh_state == 1 && k < n) {
-            nh = ld_node<int4>(S, nxt, NODE_NENT);
-            nh_state = 2;
         }
     }
     return res;
