@@ -42,7 +42,8 @@ def test_struct_layouts_match_header(tmp_path):
                     'sizeof(rt_update_stats),offsetof(rt_config_desc,sky_image),sizeof(rt_ctx_info),'
                     'offsetof(rt_create_desc,devices));'
                     'printf("%zu %zu %zu\\n",sizeof(rt_edit_desc),offsetof(rt_edit_desc,scatter),'
-                    'offsetof(rt_edit_desc,substance_ri));return 0;}\n')
+                    'offsetof(rt_edit_desc,substance_ri));'
+                    'printf("%zu %zu %d\\n",sizeof(rt_light),offsetof(rt_light,rgb),RT_MAX_LIGHTS);return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
@@ -51,7 +52,8 @@ def test_struct_layouts_match_header(tmp_path):
             C.sizeof(abi.rt_entity_in), abi.rt_scene_desc.substance_ri.offset, C.sizeof(abi.rt_exposure_stats),
             C.sizeof(abi.rt_image_desc), abi.rt_scene_desc.images.offset, C.sizeof(abi.rt_update_stats),
             abi.rt_config_desc.sky_image.offset, C.sizeof(abi.rt_ctx_info), abi.rt_create_desc.devices.offset,
-            C.sizeof(abi.rt_edit_desc), abi.rt_edit_desc.scatter.offset, abi.rt_edit_desc.substance_ri.offset]
+            C.sizeof(abi.rt_edit_desc), abi.rt_edit_desc.scatter.offset, abi.rt_edit_desc.substance_ri.offset,
+            C.sizeof(abi.rt_light), abi.rt_light.rgb.offset, abi.RT_MAX_LIGHTS]
     assert got == want
 
 
@@ -66,6 +68,7 @@ def test_null_arguments_are_rejected_without_gpu():
     assert lib.rt_trace_frame_device(None, None, None, None, None) == abi.RT_E_INVALID
     assert lib.rt_frame_fault(None, None) == abi.RT_E_INVALID
     assert lib.rt_ctx_info_get(None, None) == abi.RT_E_INVALID
+    assert lib.rt_set_lights(None, None, 0, 0.0) == abi.RT_E_INVALID
 
 
 def test_create_rejects_bad_device_lists_without_gpu():

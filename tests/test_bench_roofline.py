@@ -54,3 +54,29 @@ def test_hbm_frame_of_survey_8d_is_not_applicable():
     assert h["reference_equivalent_TBps"] == pytest.approx(ref / 2.2197e-3 / 1e12, rel=1e-2)
     assert h["reference_equivalent_frac_of_peak"] > 1            # above HBM peak: not a bandwidth roof
     assert h["hbm_counted_frac_of_peak"] == pytest.approx(502e6 / 2.2197e-3 / 8e12, rel=1e-2)
+
+
+def test_lights_option_reaches_every_context_and_the_profiled_child():
+    """bench.py --lights K (shadow rays, a build extension): the contexts get the first K bench
+    lights, the rocprofv3 child is started with the same K, and K = 0 leaves contexts untouched."""
+    import types
+
+    calls = []
+
+    class Ctx:
+        def set_lights(self, lights, ambient):
+            calls.append((list(lights), ambient))
+
+    saved = list(bench.LIGHTS_ON)
+    try:
+        bench.LIGHTS_ON[:] = []
+        assert bench.with_lights(Ctx()) is not None and calls == []
+        bench.LIGHTS_ON[:] = bench.BENCH_LIGHTS[:2]
+        bench.with_lights(Ctx())
+        assert calls == [(bench.BENCH_LIGHTS[:2], bench.BENCH_AMBIENT)]
+        cmd = bench._child_cmd(types.SimpleNamespace(config="config5", stripe=8, lights=2))
+        assert cmd[cmd.index("--lights") + 1] == "2"
+        cmd = bench._child_cmd(types.SimpleNamespace(config="config3", stripe=8))     # older callers
+        assert cmd[cmd.index("--lights") + 1] == "0"
+    finally:
+        bench.LIGHTS_ON[:] = saved
