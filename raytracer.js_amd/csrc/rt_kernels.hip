@@ -2634,6 +2634,73 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
 // slot q of the frame's candidate buffers, free once k_cont is done.
 constexpr int32_t SHADOW_NO_RAY = -2;             // cand_n: this light is skipped for the record
 
+// Record q's shadow ray toward lt after its walk (cn = its cand_n): the first hit in its list decides,
+// and an unblocked light's term is added to the record's factor.
+__device__ __forceinline__ void shadow_decide(const RtLaunch &L, const RtDevScene &S, bool cull, const rt_light &lt,
+                                              RtShadowRec &e, const double o[3], const double d[3], double dist,
+                                              double cosine, int cn, uint32_t stride, uint32_t q, Counters &c)
+{
+    bool blocked;
+    if (cn < 0) {                                     // the list overflowed: the walk itself
+        blocked = shadow_blocked(S, cull, o, d, dist, c);
+    } else {
+        const int2 res = scan_first<true>(L, S, o, d, make_raybox(o, d), stride, q, cn >> 2, c);
+        if (res.y < 0) {
+            blocked = (cn & 3) != 0;                  // the walk threw or reached the step cap
+        } else {
+            const RtPrim &pr = S.prim[res.y];
+            Hit h;
+            if (prim_hit(pr, o, d, h) < 0) blocked = true;                  // the winner throws
+            else if (S.shades[pr.meta >> 2].light) blocked = false;
+            else {
+                const double a = h.p[0] - o[0], b = h.p[1] - o[1], f = h.p[2] - o[2];
+                blocked = sqrt(dot3(a, b, f, a, b, f)) < dist - 1e-3;
+            }
+        }
+    }
+    if (!blocked) {
+        double s3[3] = {e.s[0], e.s[1], e.s[2]};
+        shadow_add(L, lt, e.path, dist, cosine, s3);
+        e.s[0] = s3[0]; e.s[1] = s3[1]; e.s[2] = s3[2];
+    }
+}
+
+// RT_SHADOW_WF = 1: one kernel per light, the record's walk and its first-hit scan in the same
+// lane (lists still cache-resident), as k_walk_first does for level 0; 0 (default): two passes per light
+#ifndef RT_SHADOW_WF
+#define RT_SHADOW_WF 0
+#endif
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_shadow_wf(RtLaunch L)
+{
+    TL_SCOPE(L.tl);
+    const int lane = threadIdx.x & 63;
+    const int n = L.ctr[2];
+    const RtFrameSetup F = *L.setup;
+    const RtDevScene &S = L.scene;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    const bool cull = L.cull != 0;
+    const rt_light lt = L.lights[L.shadow_light];
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    stage_top(S);
+    for (;;) {
+        const int base = claim(L.ctr + RT_CTR_SHADOW + 2 * L.shadow_light, lane) * 64;
+        if (base >= n) break;
+        const int q = base + lane;
+        if (q >= n) continue;
+        RtShadowRec &e = L.shadow_q[q];
+        RaySrc src;
+        double dist, cosine;
+        if (!shadow_ray(lt, e.p, e.n, src.o, src.d, dist, cosine)) continue;
+        src.valid = true;
+        src.id = (size_t)q;
+        src.pix = e.pix;
+        src.rec = L.ovf;                          // non-null: seated like a continuation
+        const int cn = walk_item(L, S, F, src, stride, c);
+        shadow_decide(L, S, cull, lt, e, src.o, src.d, dist, cosine, cn, (uint32_t)stride, (uint32_t)q, c);
+    }
+}
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_shadow_walk(RtLaunch L)
 {
@@ -2687,29 +2754,7 @@ __global__ void __launch_bounds__(256, MINW) k_shadow_first(RtLaunch L)
         RtShadowRec &e = L.shadow_q[q];
         double o[3], d[3], dist, cosine;
         shadow_ray(lt, e.p, e.n, o, d, dist, cosine);
-        bool blocked;
-        if (cn < 0) {                                 // the list overflowed: the walk itself
-            blocked = shadow_blocked(S, cull, o, d, dist, c);
-        } else {
-            const int2 res = scan_first<true>(L, S, o, d, make_raybox(o, d), (uint32_t)stride, (uint32_t)q, cn >> 2, c);
-            if (res.y < 0) {
-                blocked = (cn & 3) != 0;              // the walk threw or reached the step cap
-            } else {
-                const RtPrim &pr = S.prim[res.y];
-                Hit h;
-                if (prim_hit(pr, o, d, h) < 0) blocked = true;              // the winner throws
-                else if (S.shades[pr.meta >> 2].light) blocked = false;
-                else {
-                    const double a = h.p[0] - o[0], b = h.p[1] - o[1], f = h.p[2] - o[2];
-                    blocked = sqrt(dot3(a, b, f, a, b, f)) < dist - 1e-3;
-                }
-            }
-        }
-        if (!blocked) {
-            double s3[3] = {e.s[0], e.s[1], e.s[2]};
-            shadow_add(L, lt, e.path, dist, cosine, s3);
-            e.s[0] = s3[0]; e.s[1] = s3[1]; e.s[2] = s3[2];
-        }
+        shadow_decide(L, S, cull, lt, e, o, d, dist, cosine, cn, (uint32_t)stride, (uint32_t)q, c);
     }
 }
 
@@ -3006,8 +3051,12 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             for (int l = 0; l < L.n_lights; l++) {
                 RtLaunch Ls = Lc;
                 Ls.shadow_light = l;
-                launch_persistent(k_shadow_walk<4>, st, Ls);
-                launch_persistent(k_shadow_first<4>, st, Ls);
+                if (RT_SHADOW_WF) {
+                    launch_persistent(k_shadow_wf<4>, st, Ls);
+                } else {
+                    launch_persistent(k_shadow_walk<4>, st, Ls);
+                    launch_persistent(k_shadow_first<4>, st, Ls);
+                }
             }
             launch_persistent(k_shadow<8>, st, Lc);
         }
@@ -3066,7 +3115,7 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *na
             {(const void *)k_first_refill<6>, "k_first_refill"}, {(const void *)k_first_seg<4>, "k_first_seg"},
             {(const void *)k_shade<3>, "k_shade"}, {(const void *)k_shade<4>, "k_shade"}, {(const void *)k_shade<5>, "k_shade"},
             {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<8>, "k_shadow"},
-            {(const void *)k_shadow_walk<4>, "k_shadow_walk"}, {(const void *)k_shadow_first<4>, "k_shadow_first"}};
+            {(const void *)k_shadow_walk<4>, "k_shadow_walk"}, {(const void *)k_shadow_wf<4>, "k_shadow_wf"}, {(const void *)k_shadow_first<4>, "k_shadow_first"}};
         for (int i = 0; i < n; i++) {
             for (int q = 0; q < 4; q++) rec4[4 * i + q] = v[4 * i + q];
             const char *nm = "?";
