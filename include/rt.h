@@ -354,9 +354,9 @@ int  rt_debug_rccl_frames(int32_t n_dev, int32_t n_ctx, int32_t frames, int32_t 
 
 /* ---- device-resident exposure buffer: statistics and tone mapping ---- */
 typedef struct rt_exposure_stats {
-    double mean;       /* ExposureBuffer.get_mean()              src/view/exposure_buffer.ts:90-104  */
-    double variance;   /* ExposureBuffer.get_variance(mean)      src/view/exposure_buffer.ts:106-120 */
-    double absdev;     /* ExposureBuffer.get_absolute_dev(mean)  src/view/exposure_buffer.ts:122-136 */
+    double mean;       /* ExposureBuffer.get_mean()              src/view/exposure_buffer.ts:93-108  */
+    double variance;   /* ExposureBuffer.get_variance(mean)      src/view/exposure_buffer.ts:110-125 */
+    double absdev;     /* ExposureBuffer.get_absolute_dev(mean)  src/view/exposure_buffer.ts:127-142 */
 } rt_exposure_stats;
 
 /* Luminance statistics (Y = 0.299 R + 0.587 G + 0.114 B per pixel, in binary64) of the DEVICE

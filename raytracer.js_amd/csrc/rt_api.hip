@@ -104,6 +104,7 @@ struct rt_ctx {
     bool bvh_sah = true;             // SAH splits (RT_BVH_SAH=0: median split)
     bool split = true;               // walk pass + test pass (RT_SPLIT=0: fused k_trace)
     int n_lights = 0;                // rt_set_lights: shadow rays (a build extension; 0 = off)
+    int stream_gated = 0;            // host frames the streaming gate declined since dev[0]'s last count
     double ambient = 0;
     rt_light lights[RT_MAX_LIGHTS] = {};
     uint64_t lights_seq = 0;         // bumped per rt_set_lights; a device uploads at its next frame
@@ -579,6 +580,25 @@ static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_confi
 // d.b_rgb / d.b_hit_* unless the caller repoints L.rgb.  Device d must be current.
 enum { WANT_IDS = 1, WANT_STATUS = 2 };
 
+// The newest completed counter copy of device d into its snapshot (the grid hints and the host-frame
+// streaming gate read it).  A frame that took a buffer but sent no counters (fused small frame, empty
+// part, an error before the copy) never records its event, and the query then reports success: the
+// buffer still holds the -1 prepare gave it (a copied ctr[0], the overflow count, is >= 0), and the
+// snapshot keeps the last real counts.
+static void fold_counts(RtDevice &d)
+{
+    if (!d.h_ctr) return;
+    for (int i = 0; i < 2; i++)
+        if (d.ctr_pend[i] && hipEventQuery(d.ctr_ev[i]) == hipSuccess) {
+            d.ctr_pend[i] = false;
+            if (d.ctr_seq[i] > d.ctr_snap_seq && d.h_ctr[(size_t)i * RT_CTR_INTS] >= 0) {
+                memcpy(d.ctr_snap.data(), d.h_ctr + (size_t)i * RT_CTR_INTS, sizeof(int32_t) * RT_CTR_INTS);
+                d.ctr_snap_seq = d.ctr_seq[i];
+            }
+        }
+    (void)hipGetLastError();                                                // hipErrorNotReady
+}
+
 // A part's launch: its rows are the part's stripes (rt_part_rows), or, for a band (band_rows >= 0),
 // frame rows row0 .. row0 + band_rows - 1.
 static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_config_desc *cfg, int part,
@@ -620,19 +640,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
             d.ctr_snap.assign(RT_CTR_INTS, -1);                             // unknown until a frame completes
             std::fill(d.h_ctr, d.h_ctr + 2 * RT_CTR_INTS, -1);
         }
-        // a frame that took a buffer but sent no counters (fused small frame, empty part, an error
-        // before the copy) never records its event, and the query then reports success: the buffer
-        // still holds the -1 it was given below (a copied ctr[0], the overflow count, is >= 0), and
-        // the snapshot keeps the last real counts
-        for (int i = 0; i < 2; i++)
-            if (d.ctr_pend[i] && hipEventQuery(d.ctr_ev[i]) == hipSuccess) {
-                d.ctr_pend[i] = false;
-                if (d.ctr_seq[i] > d.ctr_snap_seq && d.h_ctr[(size_t)i * RT_CTR_INTS] >= 0) {
-                    memcpy(d.ctr_snap.data(), d.h_ctr + (size_t)i * RT_CTR_INTS, sizeof(int32_t) * RT_CTR_INTS);
-                    d.ctr_snap_seq = d.ctr_seq[i];
-                }
-            }
-        (void)hipGetLastError();                                            // hipErrorNotReady
+        fold_counts(d);
         // this frame's counters go to a buffer without a transfer in flight; with both busy (frames in
         // flight) the frame sends none: any recent frame's counts will do for the hints, and a small
         // part's frame then no longer pays a copy per frame
@@ -1085,12 +1093,17 @@ static int trace_frame_stream(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     // level 1 or k_cont: config 3 ~1 %): the late list and its host patch are per pixel, and a frame
     // whose bounce levels rewrite most pixels (config 5: millions) is faster copied once at its end
     if (c->late_cap <= 0) {
+        fold_counts(d0);
         const int32_t *h = d0.ctr_snap.empty() ? nullptr : d0.ctr_snap.data();
         const long long late_hint = h && h[4] >= 0 && h[0] >= 0 ? (long long)h[4] + h[0] : -1;
         if (late_hint < 0 || late_hint * 32 > (long long)P) {
-            *no_hint = late_hint < 0;
+            // no count yet, or every 8th declined frame: the frame runs as one launch on dev[0], whose
+            // counters the gate reads next (the bands path keeps its own), so a scene or camera that
+            // changed since is seen again
+            *no_hint = c->hints && (late_hint < 0 || ++c->stream_gated % 8 == 0);
             return RT_OK;
         }
+        c->stream_gated = 0;
     }
     if ((r = prepare(c, d0, cam, cfg, 0, 1, H, WANT_STATUS | (ids ? WANT_IDS : 0), L)) != RT_OK) return r;
     if (!L.cand) return RT_OK;                                          // fused: not streamable
@@ -1310,7 +1323,9 @@ extern "C" int rt_trace_frame(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     const bool blend = cfg->col_weight != 1.0;
     FrameOut o = {};
     bool no_hint = false;
-    if (c->gather == RT_GATHER_NONE && !stats && c->host_stream && c->split && (int64_t)P >= c->stream_min) {
+    // (not with shadow lights: their matte ends are written by k_shadow after level 0, i.e. late)
+    if (c->gather == RT_GATHER_NONE && !stats && c->host_stream && c->split && !c->n_lights &&
+        (int64_t)P >= c->stream_min) {
         bool done = false;
         r = trace_frame_stream(c, cam, cfg, rgb_inout, hit_entity, hit_node, status, &done, &no_hint);
         if (r != RT_OK || done) return r;

@@ -91,7 +91,6 @@ struct RtDevScene {
     int32_t exact_slots;        // every node's slot planes equal its slot positions (dyadic cubes): the
                                 // walker takes them without recomputing the Box centre (rt_kernels.hip)
     int32_t n_top;              // slots [0, n_top) hold the upper levels breadth-first (RT_TOP_LEVELS; else 0)
-    int32_t n_lds;              // walk kernels: slots [0, n_lds) are read from the workgroup's LDS copy
     int32_t bvh_leaf;           // cull-hierarchy leaves hold up to this many entities (a node with no more
                                 // entities is one leaf: its prims at node_ent.x in order)
 };

@@ -28,9 +28,6 @@ namespace {
 
 constexpr int ST_OK = 0, ST_WARN = 1, ST_FAULT = 2, ST_CAP = 3;
 constexpr int ST_DEFER = 100;                    // split path: continuation queued, pixel written later
-#ifndef RT_EARLY_SHADE
-#define RT_EARLY_SHADE 1
-#endif
 constexpr int STEP_CAP = 1 << 24;                // per-walk loop bound: every lane terminates
 
 // RT_TL builds (-DRT_TL=1, tools/tl_probe.py): a device-side timeline of every launch, for the
@@ -81,90 +78,12 @@ __device__ __forceinline__ T ld_at(const void *base, uint32_t off)
 __device__ __forceinline__ uint32_t node_off(int n) { return (uint32_t)n << 7; }
 enum : uint32_t { NODE_CHILD = 32, NODE_BOX = 64, NODE_NENT = 96, NODE_UP = 112 };
 
-// LDS staging of the upper octree levels (build with -DRT_LDS_TOP=K, scene uploaded
-// with RT_TOP_LEVELS): a walk kernel copies node slots [0, S.n_lds) — the levels every ray crosses,
-// breadth-first — into its workgroup's LDS once, and node reads of those slots are served there.
-// S.n_lds is min(n_top, K) for the walk kernels' launches and 0 for every other kernel.
-// The copy lives in dynamic LDS (S.n_lds * 128 bytes, given at the walk kernels' launches), so no
-// other kernel's occupancy pays for it.
-#ifndef RT_LDS_TOP
-#define RT_LDS_TOP 0
-#endif
-#if RT_LDS_TOP
-extern __shared__ RtNode s_top[];
-#endif
-
-// RT_BUF_LOADS: node records through raw buffer loads (a V# over the node array in SGPRs, the 32-bit
-// record offset in one VGPR, the field in the instruction's offset): no 64-bit address arithmetic.
-#ifndef RT_BUF_LOADS
-#define RT_BUF_LOADS 0
-#endif
-#if RT_BUF_LOADS
-#ifndef RT_FS_BUFFER
-#define RT_FS_BUFFER 1                          // k_frame_start's row stores: buffer stores (1) / pointers (0)
-#endif
-typedef unsigned int rt_u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int rt_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const RtDevScene &S)
-{
-    // raw buffer (stride 0), the whole 4 GB offset range, gfx9 dword3 (as ck_tile's gfx9 resources)
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<RtNode *>(S.node), (short)0, (int)0xffffffff, 0x00020000);
-}
-template <typename T>
-__device__ __forceinline__ T buf_ld(const RtDevScene &S, uint32_t voff, uint32_t field)
-{
-    static_assert(sizeof(T) == 4 || sizeof(T) == 8 || sizeof(T) == 16, "buffer load size");
-    T v;
-    if constexpr (sizeof(T) == 4) {
-        const unsigned int x = __builtin_amdgcn_raw_buffer_load_b32(node_rsrc(S), (int)(voff + field), 0, 0);
-        __builtin_memcpy(&v, &x, 4);
-    } else if constexpr (sizeof(T) == 8) {
-        const rt_u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(node_rsrc(S), (int)(voff + field), 0, 0);
-        __builtin_memcpy(&v, &x, 8);
-    } else {
-        const rt_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(node_rsrc(S), (int)(voff + field), 0, 0);
-        __builtin_memcpy(&v, &x, 16);
-    }
-    return v;
-}
-#endif
-
+// Node reads stay in the global path: LDS staging of the upper levels (round 3) and raw buffer loads
+// measured slower or neutral (git history keeps both).
 template <typename T>
 __device__ __forceinline__ T ld_node(const RtDevScene &S, int n, uint32_t field)
 {
-#if RT_LDS_TOP
-    if ((unsigned)n < (unsigned)S.n_lds)
-        return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(s_top) + node_off(n) + field);
-#endif
-#if RT_BUF_LOADS
-    if constexpr (sizeof(T) == 32) {          // the cube: two 16-byte loads
-        T v;
-        const rt_u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(node_rsrc(S), (int)(node_off(n) + field), 0, 0);
-        const rt_u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(node_rsrc(S), (int)(node_off(n) + field + 16), 0, 0);
-        __builtin_memcpy(&v, &a, 16);
-        __builtin_memcpy(reinterpret_cast<char *>(&v) + 16, &b, 16);
-        return v;
-    } else {
-        return buf_ld<T>(S, node_off(n), field);
-    }
-#else
     return ld_at<T>(S.node, node_off(n) + field);
-#endif
-}
-
-// a walk kernel's prologue: the workgroup's copy of slots [0, S.n_lds)
-__device__ __forceinline__ void stage_top(const RtDevScene &S)
-{
-#if RT_LDS_TOP
-    if (S.n_lds > 0) {
-        const int4 *src = reinterpret_cast<const int4 *>(S.node);
-        int4 *dst = reinterpret_cast<int4 *>(s_top);
-        for (int i = threadIdx.x; i < S.n_lds * 8; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
-    }
-#else
-    (void)S;
-#endif
 }
 
 __device__ __forceinline__ NodeDims node_dims(const RtDevScene &S, int n)
@@ -187,16 +106,12 @@ __device__ __forceinline__ int4 node_up4(const RtDevScene &S, int n) { return ld
 struct RayBox;
 __device__ __forceinline__ bool node_candidate(const RtDevScene &S, int n, bool cull, const RayBox &rb);
 
-// Candidate lists are k-major [cand_cap][rays] int32, or ray-major [rays][cand_cap] on the levels
-// RT_CAND_LAYOUT selects (1: bounce levels, 2: every level); cand_cap * rays * 4 < 2^32 is ensured
-// by the host (prepare caps cand_cap), so the address is a 32-bit offset from the uniform base.
-#ifndef RT_CAND_LAYOUT
-#define RT_CAND_LAYOUT 0
-#endif
-__device__ __forceinline__ uint32_t cand_off(const RtLaunch &L, int k, uint32_t stride, uint32_t ray)
+// Candidate lists are k-major [cand_cap][rays] int32 (ray-major lists measured slower, §5.18);
+// cand_cap * rays * 4 < 2^32 is ensured by the host (prepare caps cand_cap), so the address is a
+// 32-bit offset from the uniform base.
+__device__ __forceinline__ uint32_t cand_off(const RtLaunch &, int k, uint32_t stride, uint32_t ray)
 {
-    const bool rm = RT_CAND_LAYOUT == 2 || (RT_CAND_LAYOUT == 1 && L.level >= 1);
-    return (rm ? ray * (uint32_t)L.cand_cap + (uint32_t)k : (uint32_t)k * stride + ray) << 2;
+    return ((uint32_t)k * stride + ray) << 2;
 }
 __device__ __forceinline__ void cand_store(const RtLaunch &L, int k, uint32_t stride, uint32_t ray, int node)
 {
@@ -369,9 +284,6 @@ __device__ bool reseat_throws(const RtDevScene &S, const double p[3], const doub
     return fi < 0;
 }
 
-#ifndef RT_DIV_FMA
-#define RT_DIV_FMA 0
-#endif
 // The exit half of Box.line_intersection (src/math/intersection.ts:150-204) for a walker slot:
 // u2 = the first minimum over exit faces of q/p and the emptiness check u1 > u2, bit-identical to
 // six IEEE divisions.  Exactly one face per axis is an exit face (isNegative(p) selects entering),
@@ -416,17 +328,8 @@ __device__ __forceinline__ bool slot_exit(const double tl[3], const double top[3
         const int k = s0 ? 0 : (s1 ? 1 : 2);
         const double q = s0 ? qe[0] : (s1 ? qe[1] : qe[2]);
         const double dk = s0 ? w.d[0] : (s1 ? w.d[1] : w.d[2]);
-#if RT_DIV_FMA
-        // RN(q/|d|) without the division: y = RN(q r) with r = RN(1/|d|) is within one ulp of q/|d|,
-        // the remainder q - |d| y is then exact (one FMA), and RN(y + r (q - |d| y)) is the correctly
-        // rounded quotient (Markstein's theorem) while nothing underflows or overflows — the guard
-        const double r = fabs(s0 ? w.inv[0] : (s1 ? w.inv[1] : w.inv[2]));
-        const double y = q * r;
-        if (fabs(q) >= 0x1p-900 && fabs(y) >= 0x1p-960 && fabs(y) <= 0x1p+960) u2 = fma(fma(-y, fabs(dk), q), r, y);
-        else u2 = q / fabs(dk);
-#else
+        // (the FMA-corrected reciprocal instead of the division measured slower twice, §5.16)
         u2 = q / fabs(dk);                                   // (neg ? -d : d), bit for bit unless NaN
-#endif
         i2 = 2 * k + (signbit(dk) ? 0 : 1);
     }
     if (!(u2 < INFINITY)) { u2 = INFINITY; i2 = -1; }          // (a finite survivor never gets here)
@@ -602,27 +505,14 @@ __device__ __forceinline__ int walker_next(const RtDevScene &S, Walker &w, int &
 // A trip is the head (trip_head: the slot's child id and parent link, the emit of a node returned on
 // entry, and the classification of the lane's next action), then the action (trip_step).
 enum : int { A_NONE = 0, A_STEPIN = 1, A_EXIT = 2, A_MOVE = 3 };
-#ifndef RT_CLIMB
-#define RT_CLIMB 2
-#endif
-#ifndef RT_PEEK
-#define RT_PEEK 1
-#endif
 
-#ifndef RT_HEAD_LEAN
-#define RT_HEAD_LEAN 1
-#endif
 template <bool STOP, typename Emit>
 __device__ __forceinline__ void trip_head(const RtDevScene &S, Walker &w, Emit &&emit, int stop, int &res, int &act,
                                           int &lnode, int4 &up)
 {
     act = A_NONE;
-#if !RT_HEAD_LEAN
-    lnode = -1;
-    up = make_int4(-1, RT_OCT_UNDEF, -1, RT_OCT_UNDEF);
-#endif
-    // (RT_HEAD_LEAN: lnode / up are read by trip_step only for the actions that set them here, so
-    // the early exits below need no defaults, and the compiler no copies of them per exit)
+    // lnode / up are read by trip_step only for the actions that set them here, so the early exits
+    // below need no defaults, and the compiler no copies of them per exit (§5.16)
     if (res != 1) return;
     const int ltree = w.cur_tree, loct = w.cur_oct;
     if (++w.steps > STEP_CAP) {
@@ -633,10 +523,6 @@ __device__ __forceinline__ void trip_head(const RtDevScene &S, Walker &w, Emit &
         if (loct != RT_OCT_UNDEF) {
             lnode = node_child(S, ltree, loct);
             up = node_up4(S, ltree);                       // parent and grandparent links, same line
-#if RT_CLIMB < 2
-            up.z = -1;
-            up.w = RT_OCT_UNDEF;
-#endif
         } else {
             lnode = ltree;
         }
@@ -673,7 +559,6 @@ __device__ __forceinline__ void trip_step(const RtDevScene &S, Walker &w, int &r
             w.cur_oct = oct;
             w.flags &= ~F_RET;
             act = A_NONE;
-#if RT_PEEK
             // The next iteration at the entered slot, from the line whose cube was
             // just read: an empty slot (not a segment's stop cell) is not returned and goes to its
             // exit, whose cube is this one: take that iteration now, with its step.  A node in the
@@ -682,14 +567,9 @@ __device__ __forceinline__ void trip_step(const RtDevScene &S, Walker &w, int &r
                 if (node_child(S, lnode, oct) < 0 && !(STOP && lnode * 8 + oct == stop)) {
                     w.steps++;
                     up = node_up4(S, lnode);
-#if RT_CLIMB < 2
-                    up.z = -1;
-                    up.w = RT_OCT_UNDEF;
-#endif
                     act = A_EXIT;
                 }
             }
-#endif
         }
         if (act == A_EXIT) {
             Counters c_unused;
@@ -717,7 +597,6 @@ __device__ __forceinline__ void trip_step(const RtDevScene &S, Walker &w, int &r
                 else w.flags &= ~F_RET;
                 if (up.x >= 0) { w.cur_tree = up.x; w.cur_oct = up.y; }
                 else w.cur_oct = RT_OCT_UNDEF;
-#if RT_CLIMB
                 // The next iteration at the parent slot: its child is the node just
                 // left (already returned: F_RET, depth was > 0), F_AHEAD moves it along the same normal
                 // again.  When that move is a sibling move it needs no load: do it now, with its step.
@@ -729,9 +608,7 @@ __device__ __forceinline__ void trip_step(const RtDevScene &S, Walker &w, int &r
                         w.steps++;
                         w.cur_oct = (up.y & ~(1 << axis)) | (nb2 << axis);
                         w.flags = 0;
-                    }
-#if RT_CLIMB >= 2
-                    else {
+                    } else {
                         // that move is a step_back too: with the grandparent link (up.z, up.w) of the
                         // same record, take it, and the grandparent slot's sibling move when it is one
                         w.steps++;                                 // the parent slot's iteration
@@ -747,9 +624,7 @@ __device__ __forceinline__ void trip_step(const RtDevScene &S, Walker &w, int &r
                             w.flags = 0;
                         }
                     }
-#endif
                 }
-#endif
             }
         }
     }
@@ -764,9 +639,6 @@ __device__ __forceinline__ void walker_trip(const RtDevScene &S, Walker &w, Emit
     trip_step<STOP, ALL_FAST>(S, w, res, act, lnode, up, stop);
 }
 
-#ifndef RT_TRIP_UNROLL
-#define RT_TRIP_UNROLL 1
-#endif
 #ifndef RT_WALK_PROF
 #define RT_WALK_PROF 0
 #endif
@@ -813,8 +685,7 @@ __device__ __forceinline__ int walker_run_t(const RtDevScene &S, Walker &w, Emit
     pf.flush();
 #else
     do {
-#pragma unroll
-        for (int u = 0; u < RT_TRIP_UNROLL; u++) walker_trip<STOP, ALL_FAST>(S, w, emit, stop, res);
+        walker_trip<STOP, ALL_FAST>(S, w, emit, stop, res);   // (2-4 trips per ballot: neutral, §5.12a)
     } while (__ballot(res == 1));
 #endif
     return res;
@@ -991,15 +862,10 @@ __device__ __forceinline__ bool ray_box(const RtBvh &b, const RayBox &rb)
     return tmin <= tmax;
 }
 
-// RT_EMIT_BOX = 0 (A/B variant): the walk pass keeps every node with entities and the first-hit pass
-// tests the cull-root box itself (the walker's trips lose the slab test, the lists grow)
-#ifndef RT_EMIT_BOX
-#define RT_EMIT_BOX 1
-#endif
 __device__ __forceinline__ bool node_candidate(const RtDevScene &S, int n, bool cull, const RayBox &rb)
 {
     if (ld_node<int32_t>(S, n, NODE_NENT) == 0) return false;
-    if (!RT_EMIT_BOX || !cull || !rb.ok) return true;
+    if (!cull || !rb.ok) return true;
     const float4 lo = ld_node<float4>(S, n, NODE_BOX);              // lo.xyz, hi.x
     const float2 hi = ld_node<float2>(S, n, NODE_BOX + 16);         // hi.yz
     RtBvh b;
@@ -1079,7 +945,7 @@ __device__ __forceinline__ int node_first_hit(const RtDevScene &S, const int4 ne
 
 // A ray's candidate scan (the first-hit pass): the first node of its list, in walk order, with an
 // exact hit, and the winning prim slot — node_first_hit over list[0..n) until one hits.
-// RT_SCAN_FLAT = 1: one loop for the whole scan.  A trip is one cull-hierarchy record, or one leaf
+// One loop for the whole scan (FLAT).  A trip is one cull-hierarchy record, or one leaf
 // prim's exact test, or the step to the next candidate, so a lane whose traversal of one node ended
 // goes on to its next candidate at once instead of waiting, at the end of every node, for the
 // wave's longest traversal (the nested loops pay the sum over candidates of the wave's maximum; this
@@ -1087,18 +953,12 @@ __device__ __forceinline__ int node_first_hit(const RtDevScene &S, const int4 ne
 // ray: identical results.  Rays that cannot be culled (rb.ok false) keep the nested scan.
 // k_walk_first keeps the nested scan (FLAT = false): behind the walk in the same wave it measured 1 %
 // faster there.
-#ifndef RT_SCAN_FLAT
-#define RT_SCAN_FLAT 1
-#endif
-#ifndef RT_SCAN_PF
-#define RT_SCAN_PF 1                              // next candidate id one node ahead (profiles/r4_v4/ab)
-#endif
 template <bool FLAT = true>
 __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &S, const double o[3], const double d[3],
                                            const RayBox &rb, uint32_t stride, uint32_t id, int n, Counters &c)
 {
     int2 res = make_int2(-1, -1);
-    if (!FLAT || !RT_SCAN_FLAT || !(L.cull != 0 && rb.ok)) {
+    if (!FLAT || !(L.cull != 0 && rb.ok)) {
         for (int k = 0; k < n; k++) {
             const int node = cand_load(L, k, stride, id);
             const int4 hdr = ld_node<int4>(S, node, NODE_NENT);      // {n_ent, ent_begin, bvh_root, -}
@@ -1106,7 +966,7 @@ __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &
             int rank;
             long long box = 0;
             const int hk = node_first_hit<false>(S, make_int4(hdr.y, hdr.x, hdr.z, 0), o, d, rb, L.cull != 0, c, box,
-                                                 h, rank, RT_EMIT_BOX != 0);
+                                                 h, rank, true);
             if (hk >= 0) { res = make_int2(node, hk); break; }
         }
         return res;
@@ -1114,9 +974,9 @@ __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &
     // i >= 0: the next record of the current node's hierarchy; slot < prim_end: leaf prims to test
     int k = 0, node = -1, i = -1, slot = 0, prim_end = 0, best_rank = 0x7fffffff, best_slot = -1;
     bool active = n > 0;
-    // RT_SCAN_PF: the next candidate's id is loaded one node ahead, so a node switch waits for the
-    // header load only
-    int nxt = RT_SCAN_PF && n > 0 ? cand_load(L, 0, stride, id) : -1;
+    // the next candidate's id is loaded one node ahead, so a node switch waits for the header load
+    // only (profiles/r4_v4/ab)
+    int nxt = n > 0 ? cand_load(L, 0, stride, id) : -1;
     while (active) {
         if (slot < prim_end) {
             const int rk = S.prim[slot].rank;
@@ -1137,16 +997,11 @@ __device__ __forceinline__ int2 scan_first(const RtLaunch &L, const RtDevScene &
         } else if (k >= n) {
             active = false;
         } else {
-            if (RT_SCAN_PF) {
-                node = nxt;
-                k++;
-                if (k < n) nxt = cand_load(L, k, stride, id);
-            } else {
-                node = cand_load(L, k++, stride, id);
-            }
+            node = nxt;
+            k++;
+            if (k < n) nxt = cand_load(L, k, stride, id);
             const int4 hdr = ld_node<int4>(S, node, NODE_NENT);
-            if (!RT_EMIT_BOX) i = hdr.z;                   // node_first_hit's root_hit: the walk pass
-            else if (hdr.x <= S.bvh_leaf) { slot = hdr.y; prim_end = hdr.y + hdr.x; }   // crossed the
+            if (hdr.x <= S.bvh_leaf) { slot = hdr.y; prim_end = hdr.y + hdr.x; }   // crossed the
             else i = hdr.z + 1;                            // root box: a leaf root's prims, or its children
         }
     }
@@ -1180,9 +1035,6 @@ __device__ __forceinline__ int wave_min(int v)
 // at most H/2 + W/2 steps of one multiply-add pair, bit-identical to the sequential scan.
 // dirs: SoA planes [3][W*rows], x-major (index x*rows + local row): a wave stores 64 consecutive
 // rows of one column per step, and an 8x8 tile of the walk reads 8 runs of 64 bytes per plane.
-#ifndef RT_FS_BUFFER
-#define RT_FS_BUFFER 1                          // k_frame_start's row stores: buffer stores (1) / pointers (0)
-#endif
 typedef unsigned int rt_u32x2 __attribute__((ext_vector_type(2)));
 #define RT_BUFFER_DWORD3 0x00020000             // gfx9 raw buffer: 32-bit data format, no swizzle
 
@@ -1271,7 +1123,7 @@ __global__ void __launch_bounds__(64) k_frame_start(RtDevScene S, rt_camera_desc
     // address arithmetic in the chain's loop); the plane's size bounds every store.  A plane of
     // 2 GiB or more (over 2^28 pixels in the part) takes 64-bit pointers
     const size_t plane_sz = (size_t)rows * (size_t)W * sizeof(double);
-    if (!RT_FS_BUFFER || plane_sz >= ((size_t)1 << 31)) {
+    if (plane_sz >= ((size_t)1 << 31)) {
         double *p = dirs + (size_t)i * (size_t)rows * (size_t)W + (size_t)from * (size_t)rows + (size_t)lr;
         const ptrdiff_t step = (ptrdiff_t)inc * (ptrdiff_t)rows;
         for (int k = 0; k < n; k++) {
@@ -1848,7 +1700,7 @@ __device__ __forceinline__ void ray_src(const RtLaunch &L, int item, int lane, R
     }
 }
 
-// Level 0's shading queue (k_first -> k_shade, RT_EARLY_SHADE): its length, in a free slot of the
+// Level 0's shading queue (k_first -> k_shade): its length, in a free slot of the
 // level's counter block; the entries (pixel ids of this part) live in ray_cn, unused at level 0.
 __device__ __forceinline__ int32_t *shade_n(const RtLaunch &L) { return lvl_ctr(L, 0) + 1; }
 
@@ -2074,25 +1926,19 @@ __device__ __forceinline__ void seg_first_item(const RtLaunch &L, const RtDevSce
     }
 }
 
-// RT_SEG_FUSED = 1 (default): a segmented level's walk and first-hit scan run as one pass, k_seg:
+// A segmented level's walk and first-hit scan run as one pass, k_seg:
 // a wave walks its item's segments and then scans their lists, whose counts it holds in registers,
 // as k_walk_first does for level 0.  These levels are latency-bound (few, long rays), so a second
 // launch cost its own drain and, with frames in flight, a slot among the few kernels the GPU runs at
 // once (small parts).
-#ifndef RT_SEG_FUSED
-#define RT_SEG_FUSED 1
-#endif
-#ifndef RT_SEG_SHADE
-#define RT_SEG_SHADE 1                 // k_seg also shades levels of up to RT_SEG_SHADE_MAX rays (k_shade skips them)
-#endif
-#ifndef RT_SEG_SHADE_MAX
-#define RT_SEG_SHADE_MAX 32768         // = the rays k_shade would take 8 per wave (cont_g); wider levels keep
-#endif                                 // k_shade's wider waves and k_seg's 4-wave occupancy
+// k_seg also shades levels of up to RT_SEG_SHADE_MAX rays (k_shade skips them): the rays k_shade would
+// take 8 per wave (cont_g); wider levels keep k_shade's wider waves and k_seg's 4-wave occupancy
+constexpr int RT_SEG_SHADE_MAX = 32768;
 __device__ __forceinline__ void shade_ray(const RtLaunch &L, const RtFrameSetup &F, const RayQueues &Q, const RaySrc &src,
                                           int cn, int2 fh, Counters &c);
 __device__ __forceinline__ bool seg_shaded(const RtLaunch &L)
 {
-    return RT_SEG_FUSED && RT_SEG_SHADE && L.level >= 1 && seg_mode(L) && *lvl_ctr(L, L.level - 1) <= RT_SEG_SHADE_MAX;
+    return L.level >= 1 && seg_mode(L) && *lvl_ctr(L, L.level - 1) <= RT_SEG_SHADE_MAX;
 }
 // A segmented level's items: walk, scan and (SHADE) shading per work item, until the level's queue of
 // items is empty (k_seg, k_level).
@@ -2137,51 +1983,7 @@ __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     if (!seg_mode(L) || seg_shaded(L) != SHADE) return;     // the other instantiation takes this level
-    stage_top(L.scene);
     seg_level<SHADE>(L, L.seg);
-}
-
-// The two passes apart (RT_SEG_FUSED = 0).
-template <int MINW>
-__global__ void __launch_bounds__(256, MINW) k_walk_seg(RtLaunch L)
-{
-    TL_SCOPE(L.tl);
-    if (!seg_mode(L)) return;
-    stage_top(L.scene);
-    const int lane = threadIdx.x & 63;
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
-    const SegLane g = seg_lane(L, L.seg);
-    const int items = (g.n_rays + g.rpw - 1) / g.rpw;
-    for (;;) {
-        int t_end;
-        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
-        if (t >= items) break;
-        seg_walk_item(L, L.scene, g, t, stride, c);
-    }
-}
-
-template <int MINW>
-__global__ void __launch_bounds__(256, MINW) k_first_seg(RtLaunch L)
-{
-    TL_SCOPE(L.tl);
-    if (!seg_mode(L)) return;
-    const int lane = threadIdx.x & 63;
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
-    const bool fault = L.setup->fault != 0;
-    const SegLane g = seg_lane(L, L.seg);
-    const int items = (g.n_rays + g.rpw - 1) / g.rpw;
-    for (;;) {
-        int t_end;
-        const int t = claim_xcd(pass_heads(L, L.level, 2), items, lane, 1, t_end, L.xcd_mask & 2);
-        if (t >= items) break;
-        const int q = t * g.rpw + lane / g.K;
-        const int cn = q < g.n_rays ? L.cand_n[(size_t)q * g.K + g.j] : SEG_SKIP;
-        int2 out;
-        int ocn;
-        seg_first_item(L, L.scene, g, t, cn, stride, fault, c, out, ocn);
-    }
 }
 
 // Walk pass of a wide bounce level with per-lane refill (RT_REFILL = G > 0; levels of 64 rays per
@@ -2195,18 +1997,11 @@ __device__ __forceinline__ bool refill_level(const RtLaunch &L)
     return L.refill > 0 && L.level >= 1 && !seg_mode(L) && cont_g(L) == 64;
 }
 
-#ifndef RT_REFILL_FAST
-#define RT_REFILL_FAST 0              // the fast-ray trip in the refill walk: measured neutral (§5.16)
-#endif
-#ifndef RT_REFILL_OCC
-#define RT_REFILL_OCC 4               // waves per SIMD the refill walk's registers must admit
-#endif
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     if (!refill_level(L)) return;
-    stage_top(L.scene);
     constexpr int IDLE = 9;
     const int lane = threadIdx.x & 63;
     const RtDevScene &S = L.scene;
@@ -2248,14 +2043,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
             if (n < L.cand_cap) cand_store(L, n, (uint32_t)stride, (uint32_t)q, node);
             n++;
         };
-#if RT_REFILL_FAST
-        // a wave whose walking lanes all have fast rays (all of them in practice) runs the trip
-        // without the exact six-division slot exit, as k_walk's fast loop does
-        if (__all(w.fast || res != 1)) walker_trip<false, true>(S, w, emit, -1, res);
-        else walker_trip<false, false>(S, w, emit, -1, res);
-#else
-        walker_trip<false, false>(S, w, emit, -1, res);
-#endif
+        walker_trip<false, false>(S, w, emit, -1, res);   // (a fast-ray trip here: neutral, §5.16)
         if (res != 1 && res != IDLE) {
             const int end = res == 0 ? 0 : (res == -2 ? 2 : 1);
             L.cand_n[q] = n > L.cand_cap ? -1 : n * 4 + end;
@@ -2302,9 +2090,8 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (seg_mode(L) || refill_level(L)) return;       // k_walk_seg / k_walk_refill take this level
+    if (seg_mode(L) || refill_level(L)) return;       // k_seg / k_level / k_walk_refill take this level
     if (L.walk_first && L.level == 0) return;         // k_walk_first takes level 0
-    stage_top(S);
     for (;;) {
         int t_end;
         const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
@@ -2365,78 +2152,6 @@ __device__ __forceinline__ bool early_shade(const RtLaunch &L, const RaySrc &src
     return true;
 }
 
-#ifndef RT_FIRST_REFILL
-#define RT_FIRST_REFILL 0              // measured slower: lanes refilled with new rays
-#endif                                 // lose the cache locality of the rays a wave already holds
-
-// First-hit pass of a wide bounce level with per-lane refill (the levels k_walk_refill walks): a
-// lane tests one candidate node per trip; a lane whose ray is done (a hit, or its list exhausted)
-// writes first[q] and, once L.refill lanes of the wave are idle, they take the next rays of the
-// level's queue with one atomic.  Each ray's candidates are tested in list order with the same
-// node_first_hit as k_first, so first[] is identical; the rays of such a level are incoherent and
-// their lists differ in length, so a wave of 64 no longer waits for its longest list.
-template <int MINW>
-__global__ void __launch_bounds__(256, MINW) k_first_refill(RtLaunch L)
-{
-    TL_SCOPE(L.tl);
-    if (!RT_FIRST_REFILL || !refill_level(L)) return;
-    const int lane = threadIdx.x & 63;
-    const RtDevScene &S = L.scene;
-    const uint32_t stride = (uint32_t)((size_t)L.rows * (size_t)L.cam.width);
-    const int n_rays = *lvl_ctr(L, L.level - 1);
-    int32_t *head = pass_heads(L, L.level, 2);
-    const bool fault = L.setup->fault != 0;
-    const RtCont *queue = lvl_queue(L, L.level - 1);
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    int q = 0, k = 0, n = 0;
-    bool busy = false, drained = false;
-    double o[3] = {0, 0, 0}, d[3] = {0, 0, 0};
-    RayBox rb{};
-    const unsigned long long below = (1ull << lane) - 1;
-    for (;;) {
-        const unsigned long long m_busy = __ballot(busy);
-        const int idle = 64 - __popcll(m_busy);
-        if (!drained && (idle >= L.refill || !m_busy)) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(head, idle);
-            base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
-            drained = base + idle >= n_rays;
-            const int r = base + __popcll(~m_busy & below);
-            if (!busy && r < n_rays) {
-                q = r;
-                const int cn = L.cand_n[q];
-                if (cn >= 4 && !fault) {
-                    const RtCont *rec = queue + q;
-                    for (int i = 0; i < 3; i++) { o[i] = rec->o[i]; d[i] = rec->d[i]; }
-                    rb = make_raybox(o, d);
-                    n = cn >> 2;
-                    k = 0;
-                    busy = true;
-                } else {
-                    reinterpret_cast<int2 *>(L.first)[q] = make_int2(-1, -1);
-                }
-            }
-        }
-        if (!__ballot(busy)) {
-            if (drained) break;
-            continue;
-        }
-        if (busy) {
-            const int node = cand_load(L, k, stride, (uint32_t)q);
-            const int4 hdr = ld_node<int4>(S, node, NODE_NENT);      // {n_ent, ent_begin, bvh_root, -}
-            Hit h;
-            int rank;
-            long long box = 0;
-            const int hk = node_first_hit<false>(S, make_int4(hdr.y, hdr.x, hdr.z, 0), o, d, rb, L.cull != 0, c, box,
-                                                 h, rank, RT_EMIT_BOX != 0);
-            k++;
-            if (hk >= 0 || k >= n) {
-                reinterpret_cast<int2 *>(L.first)[q] = hk >= 0 ? make_int2(node, hk) : make_int2(-1, -1);
-                busy = false;
-            }
-        }
-    }
-}
 // The first-hit pass's work for one ray (k_first, k_walk_first): the first candidate of its list
 // (walk order) with an exact hit; at level 0 the plain terminal rays end here (early_shade) and the
 // others are queued for k_shade.
@@ -2455,7 +2170,7 @@ __device__ __forceinline__ void first_item(const RtLaunch &L, const RtDevScene &
 // for k_shade; first[id] = {node, slot} or {-1, -1}.
 __device__ __forceinline__ void first_finish(const RtLaunch &L, const RaySrc &src, int cn, int2 res, bool fault)
 {
-    if (RT_EARLY_SHADE && L.level == 0) {
+    if (L.level == 0) {
         // level 0: end the plain terminal rays here; queue the rest for k_shade (ray_cn is free at
         // level 0), wave by wave so a shading wave keeps a tile's rays together
         RayResult R;
@@ -2477,8 +2192,7 @@ __global__ void __launch_bounds__(256, MINW) k_first(RtLaunch L)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const bool fault = L.setup->fault != 0;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (seg_mode(L)) return;                          // k_first_seg takes this level
-    if (RT_FIRST_REFILL && refill_level(L)) return;   // k_first_refill takes this level
+    if (seg_mode(L)) return;                          // k_seg / k_level take this level
     if (L.walk_first && L.level == 0) return;         // k_walk_first took level 0
     const int ch = L.claim_chunk;
     for (;;) {
@@ -2514,7 +2228,6 @@ __global__ void __launch_bounds__(BS, MINW) k_walk_first(RtLaunch L)
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    stage_top(S);
     for (;;) {
         int t_end;
         int t = claim_xcd(head, items, lane, 1, t_end, (L.xcd_mask & 1) && !L.l0_half);
@@ -2572,7 +2285,7 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
     const RayQueues Q = {lvl_queue(L, L.level), lvl_ctr(L, L.level), L.ovf, L.ctr, L.last_level != 0};
     const int ch = L.claim_chunk;
     const int32_t *ray_cn = seg_mode(L) ? L.ray_cn : L.cand_n;     // segmented levels: k_first's combined status
-    const bool queued = RT_EARLY_SHADE && L.level == 0;             // level 0: the rays k_first queued
+    const bool queued = L.level == 0;             // level 0: the rays k_first queued
     const int n_q = queued ? *shade_n(L) : 0;
     const int n_it = queued ? (n_q + 63) >> 6 : items;
     for (;;) {
@@ -2665,42 +2378,6 @@ __device__ __forceinline__ void shadow_decide(const RtLaunch &L, const RtDevScen
     }
 }
 
-// RT_SHADOW_WF = 1: one kernel per light, the record's walk and its first-hit scan in the same
-// lane (lists still cache-resident), as k_walk_first does for level 0; 0 (default): two passes per light
-#ifndef RT_SHADOW_WF
-#define RT_SHADOW_WF 0
-#endif
-template <int MINW>
-__global__ void __launch_bounds__(256, MINW) k_shadow_wf(RtLaunch L)
-{
-    TL_SCOPE(L.tl);
-    const int lane = threadIdx.x & 63;
-    const int n = L.ctr[2];
-    const RtFrameSetup F = *L.setup;
-    const RtDevScene &S = L.scene;
-    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
-    const bool cull = L.cull != 0;
-    const rt_light lt = L.lights[L.shadow_light];
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    stage_top(S);
-    for (;;) {
-        const int base = claim(L.ctr + RT_CTR_SHADOW + 2 * L.shadow_light, lane) * 64;
-        if (base >= n) break;
-        const int q = base + lane;
-        if (q >= n) continue;
-        RtShadowRec &e = L.shadow_q[q];
-        RaySrc src;
-        double dist, cosine;
-        if (!shadow_ray(lt, e.p, e.n, src.o, src.d, dist, cosine)) continue;
-        src.valid = true;
-        src.id = (size_t)q;
-        src.pix = e.pix;
-        src.rec = L.ovf;                          // non-null: seated like a continuation
-        const int cn = walk_item(L, S, F, src, stride, c);
-        shadow_decide(L, S, cull, lt, e, src.o, src.d, dist, cosine, cn, (uint32_t)stride, (uint32_t)q, c);
-    }
-}
-
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_shadow_walk(RtLaunch L)
 {
@@ -2712,7 +2389,6 @@ __global__ void __launch_bounds__(256, MINW) k_shadow_walk(RtLaunch L)
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const rt_light lt = L.lights[L.shadow_light];
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    stage_top(S);
     for (;;) {
         const int base = claim(L.ctr + RT_CTR_SHADOW + 2 * L.shadow_light, lane) * 64;
         if (base >= n) break;
@@ -2791,7 +2467,6 @@ template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_level(RtLaunch L)
 {
     TL_SCOPE(L.tl);
-    stage_top(L.scene);
     seg_level<true>(L, seg_mode(L) ? L.seg : 1);
 }
 
@@ -2958,7 +2633,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             // mode as seg_mode / refill_level do and launches the kernels that will return with
             // NO_OP_BLOCKS blocks: a persistent pass is correct at any grid, so a wrong prediction only
             // costs time, and a small part's frame no longer dispatches full grids that do nothing.
-            int mb_plain = mb, mb_seg = mb, mb_refill = mb, mb_first = mb, mb_first_seg = mb, mb_shade = mb;
+            int mb_plain = mb, mb_seg = mb, mb_refill = mb, mb_first = mb, mb_shade = mb;
             int mb_seg_shade = mb, mb_seg_wide = mb;
             if (lv == 0 && L.shade_hint && L.ctr_hint && L.ctr_hint[5] >= 0) {
                 // level 0's shading queue of a recent frame (shade_n): 64 rays per work item, 2x headroom
@@ -2972,29 +2647,25 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
                 while (g < 64 && (long long)g * 4096 < (long long)hint) g *= 2;
                 const bool refill = !seg && Lv.refill > 0 && g >= 64;
                 if (seg) mb_plain = mb_refill = mb_first = RT_NO_OP_BLOCKS;
-                else mb_seg = mb_first_seg = RT_NO_OP_BLOCKS;
-                const bool shaded = seg && RT_SEG_FUSED && RT_SEG_SHADE && hint <= RT_SEG_SHADE_MAX;
+                else mb_seg = RT_NO_OP_BLOCKS;
+                const bool shaded = seg && hint <= RT_SEG_SHADE_MAX;
                 if (shaded) mb_shade = mb_seg_wide = RT_NO_OP_BLOCKS;   // k_seg<.., true> shades the level
                 else mb_seg_shade = RT_NO_OP_BLOCKS;
                 if (refill) mb_plain = RT_NO_OP_BLOCKS;
                 else mb_refill = RT_NO_OP_BLOCKS;
             }
-            // a narrow level predicted segmented and shaded by k_seg: one k_level launch (k_cont folded
-            // into the last level's when a recent frame had nothing for it)
+            // a narrow level predicted segmented and shaded by k_seg: one k_level launch (k_cont stays
+            // its own launch after the levels; folding it in measured slower)
             // (level_solo 2, tests: every bounce level through k_level)
             const bool solo = lv >= 1 && (L.level_solo == 2 || (L.level_solo && hint >= 0 &&
                                                                  mb_shade == RT_NO_OP_BLOCKS && RT_NO_OP_BLOCKS > 0));
             if (solo) {
-                RtLaunch Lw = Lv;
-                Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
-                launch_persistent(k_level<2>, st, Lw, mb_seg_shade, sizeof(RtNode) * (size_t)Lw.scene.n_lds);
+                launch_persistent(k_level<2>, st, Lv, mb_seg_shade);
                 HIP_TRY(hipGetLastError());
                 continue;
             }
             if (lv == 0 && walk_wait) HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)walk_wait, 0));
-            RtLaunch Lw = Lv;                         // the walk kernels read the upper levels from LDS
-            Lw.scene.n_lds = std::min<int32_t>(L.scene.n_top, RT_LDS_TOP);
-            const size_t lds = sizeof(RtNode) * (size_t)Lw.scene.n_lds;
+            RtLaunch Lw = Lv;
             if (L.walk_first && lv == 0) {
                 // one wave per block: a part of an 8-GPU frame gives each wave about one tile, and a
                 // 4-wave block would hold its SIMD slots until its slowest tile ends
@@ -3009,33 +2680,28 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
                     RtLaunch L1 = Lw, L2 = Lw;
                     L1.l0_half = 1;
                     L2.l0_half = 2;
-                    launch_persistent(kw, st, L1, mb, lds, bs);
+                    launch_persistent(kw, st, L1, mb, 0, bs);
                     HIP_TRY(hipEventRecord((hipEvent_t)L.ev_h1, st));
                     HIP_TRY(hipStreamWaitEvent(aux, (hipEvent_t)L.ev_fs, 0));
-                    launch_persistent(kw, aux, L2, mb, lds, bs);
+                    launch_persistent(kw, aux, L2, mb, 0, bs);
                     HIP_TRY(hipEventRecord((hipEvent_t)L.ev_h2, aux));
                     HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)L.ev_h2, 0));
                     Lv.late_write = 1;            // level 0's shading writes after the halves went out
                 } else {
-                    launch_persistent(kw, st, Lw, mb, lds, bs);
+                    launch_persistent(kw, st, Lw, mb, 0, bs);
                 }
             }
-            else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb_plain, lds);
+            else launch_persistent(L.occ == 5 ? k_walk<5> : (L.occ == 3 ? k_walk<3> : k_walk<4>), st, Lw, mb_plain);
             HIP_TRY(hipGetLastError());
             if (lv == 0 && walk_done) HIP_TRY(hipEventRecord((hipEvent_t)walk_done, st));
             if (lv >= 1 && L.seg > 1) {                 // one of the two runs (§5.10)
-                if (RT_SEG_FUSED) {
-                    launch_persistent(k_seg<2, false>, st, Lw, std::min(mb_seg, mb_seg_wide), lds);
-                    if (RT_SEG_SHADE) launch_persistent(k_seg<2, true>, st, Lw, std::min(mb_seg, mb_seg_shade), lds);
-                }
-                else launch_persistent(k_walk_seg<2>, st, Lw, mb_seg, lds);
+                launch_persistent(k_seg<2, false>, st, Lw, std::min(mb_seg, mb_seg_wide));
+                launch_persistent(k_seg<2, true>, st, Lw, std::min(mb_seg, mb_seg_shade));
             }
-            if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<RT_REFILL_OCC>, st, Lw, mb_refill, lds);
+            if (lv >= 1 && Lv.refill > 0) launch_persistent(k_walk_refill<4>, st, Lw, mb_refill);
             if (!(L.walk_first && lv == 0))              // k_walk_first took level 0's first-hit pass
                 launch_persistent(L.occ == 8 ? k_first<8> : (L.occ == 4 ? k_first<4> : k_first<6>), st, Lv, mb_first);
             HIP_TRY(hipGetLastError());
-            if (RT_FIRST_REFILL && lv >= 1 && Lv.refill > 0) launch_persistent(k_first_refill<6>, st, Lv, mb);
-            if (lv >= 1 && L.seg > 1 && !RT_SEG_FUSED) launch_persistent(k_first_seg<4>, st, Lv, mb_first_seg);
             launch_persistent(L.shade_occ == 5 ? k_shade<5> : (L.shade_occ == 4 ? k_shade<4> : k_shade<3>), st, Lv, mb_shade);
             HIP_TRY(hipGetLastError());
             if (lv == 0 && L.l0_done) HIP_TRY(hipEventRecord((hipEvent_t)L.l0_done, st));
@@ -3051,12 +2717,8 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             for (int l = 0; l < L.n_lights; l++) {
                 RtLaunch Ls = Lc;
                 Ls.shadow_light = l;
-                if (RT_SHADOW_WF) {
-                    launch_persistent(k_shadow_wf<4>, st, Ls);
-                } else {
-                    launch_persistent(k_shadow_walk<4>, st, Ls);
-                    launch_persistent(k_shadow_first<4>, st, Ls);
-                }
+                launch_persistent(k_shadow_walk<4>, st, Ls);
+                launch_persistent(k_shadow_first<4>, st, Ls);
             }
             launch_persistent(k_shadow<8>, st, Lc);
         }
@@ -3110,12 +2772,12 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *na
             {(const void *)k_walk<4>, "k_walk"}, {(const void *)k_walk<5>, "k_walk"},
             {(const void *)k_seg<2, false>, "k_seg_wide"}, {(const void *)k_seg<2, true>, "k_seg"},
             {(const void *)k_level<2>, "k_level"},
-            {(const void *)k_walk_seg<2>, "k_walk_seg"}, {(const void *)k_walk_refill<RT_REFILL_OCC>, "k_walk_refill"},
+            {(const void *)k_walk_refill<4>, "k_walk_refill"},
             {(const void *)k_first<4>, "k_first"}, {(const void *)k_first<6>, "k_first"}, {(const void *)k_first<8>, "k_first"},
-            {(const void *)k_first_refill<6>, "k_first_refill"}, {(const void *)k_first_seg<4>, "k_first_seg"},
+
             {(const void *)k_shade<3>, "k_shade"}, {(const void *)k_shade<4>, "k_shade"}, {(const void *)k_shade<5>, "k_shade"},
             {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<8>, "k_shadow"},
-            {(const void *)k_shadow_walk<4>, "k_shadow_walk"}, {(const void *)k_shadow_wf<4>, "k_shadow_wf"}, {(const void *)k_shadow_first<4>, "k_shadow_first"}};
+            {(const void *)k_shadow_walk<4>, "k_shadow_walk"}, {(const void *)k_shadow_first<4>, "k_shadow_first"}};
         for (int i = 0; i < n; i++) {
             for (int q = 0; q < 4; q++) rec4[4 * i + q] = v[4 * i + q];
             const char *nm = "?";

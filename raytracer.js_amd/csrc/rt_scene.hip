@@ -505,7 +505,6 @@ struct RtSceneStore {
         d.n_bvh = (int32_t)bvh_used;
         d.n_top = n_top;
         d.bvh_leaf = leaf;
-        d.n_lds = 0;                                   // set per launch for the walk kernels (rt_kernels.hip)
 #ifdef RT_NO_EXACT_SLOTS
         d.exact_slots = 0;                             // A/B builds: the general plane computation only
 #else

@@ -535,7 +535,8 @@ class Raytracer {
 		this.last_hit_entity = null;
 		this.last_hit_node = null;
 		this.last_status = null;
-		this._lights = null;            // shadow rays: sent before the next frame when not null
+		this._lights = null;            // shadow rays: the last light list (null: none set)
+		this._lights_sent = null;       // the context _lights went to (a new context gets them again)
 		if (this.options.lights) this.set_lights(this.options.lights, this.options.ambient);
 	}
 
@@ -544,6 +545,7 @@ class Raytracer {
 		const vec = (p) => (p && p.v ? p.v : p);
 		this._lights = { list: (lights || []).map((l) => ({ pos: Array.from(vec(l.pos)), rgb: Array.from(vec(l.rgb)) })),
 			ambient: +(ambient || 0) };
+		this._lights_sent = null;
 	}
 
 	set_camera(camera) { this.camera = camera; }
@@ -569,6 +571,7 @@ class Raytracer {
 		if (this._journal) { JOURNALS.delete(this._journal); this._journal = null; }
 		this._st = null;
 		if (this._ctx) { load_addon().destroy(this._ctx); this._ctx = null; }
+		this._lights_sent = null;
 	}
 
 	// After a full read of the scene: the resident slot of every node (slots: sceneSlots' map; null =
@@ -665,9 +668,10 @@ class Raytracer {
 	trace_frame() {
 		const a = load_addon();
 		const scene = this._sync_scene();
-		if (this._lights) {
+		if (this._lights && this._lights_sent !== this._ctx) {
+			// kept after sending: a context created after close() (or any new one) gets them too
 			a.setLights(this._ctx, this._lights.list, this._lights.ambient);
-			this._lights = null;
+			this._lights_sent = this._ctx;
 		}
 		const cam = camera_desc(this.camera);
 		const eb = this.ebuffer;
