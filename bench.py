@@ -88,10 +88,24 @@ PASS_BYTES = {"walk": dict(n_ret=48, n_slot=32, n_loc=40), "first": dict(n_cull=
               "shade": dict(n_hit=44, segments=36)}
 BYTES_KERNEL = dict(n_ret=48, n_slot=32, n_loc=40, n_cull=32, n_exact=80, n_hit=44, primary=36)
 BYTES_REF = dict(n_ret=48, n_slot=32, n_loc=40, n_sph=36, n_box=36, n_tri=76, n_hit=40, primary=12)
-KERNEL_PASS = {"k_walk": "walk", "k_walk_seg": "walk", "k_walk_refill": "walk", "k_first": "first",
-               "k_first_seg": "first", "k_first_refill": "first", "k_shade": "shade"}
-TRACE_KERNELS = ("k_walk_first", "k_seg", "k_walk", "k_walk_seg", "k_walk_refill", "k_first", "k_first_seg",
-                 "k_first_refill", "k_shade", "k_cont", "k_trace", "k_frame_start")
+KERNEL_PASS = {"k_walk": "walk", "k_walk_refill": "walk", "k_first": "first", "k_shade": "shade"}
+# kernels whose time is part of a frame: every __global__ of rt_kernels.hip (the frame's whole kernel
+# set, so a new kernel is never left out of the roofline table) except the debug walk
+KERNEL_SRC = os.path.join(ROOT, "raytracer.js_amd", "csrc", "rt_kernels.hip")
+
+
+def frame_kernels(path=KERNEL_SRC):
+    try:
+        with open(path) as fh:
+            src = fh.read()
+    except OSError:
+        return ("k_frame_start", "k_walk_first", "k_walk", "k_walk_refill", "k_first", "k_seg", "k_level", "k_shade",
+                "k_cont", "k_trace", "k_shadow_walk", "k_shadow_first", "k_shadow")
+    names = re.findall(r"__global__\s+void\s+(?:__launch_bounds__\([^)]*\)\s+)?(k_[A-Za-z0-9_]+)\s*\(", src)
+    return tuple(sorted(set(n for n in names if n != "k_debug_walk")))
+
+
+TRACE_KERNELS = frame_kernels()
 # Shadow rays (a build extension, include/rt.h rt_set_lights): --lights K puts the first K of these
 # point lights into every context and the oracle baseline (BASELINE config 5: "4 bounces + shadow
 # rays").  The counted segments exclude the shadow rays (rt_stats does not count them).
@@ -405,22 +419,40 @@ def kernel_durations(args, deadline, cap_s=60.0, reserve_s=0.0):
     if err:
         return None, err
     try:
-        dur = {}
-        for f in glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True):
-            with open(f) as fh:
-                for r in _after_first_frame(list(csv.DictReader(fh)), "Start_Timestamp"):
-                    k = _kernel_base(r["Kernel_Name"])
-                    if k in TRACE_KERNELS:
-                        dur[k] = dur.get(k, 0.0) + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+        dur = parse_kernel_trace(glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True))
         if args.profile_out:
             os.makedirs(args.profile_out, exist_ok=True)
             for f in glob.glob(os.path.join(out, "**", "*kernel_stats.csv"), recursive=True):
                 shutil.copy(f, os.path.join(args.profile_out, "kernel_stats_%s.csv" % args.config))
         if not dur:
             return None, "kernel trace: no trace-kernel rows"
-        return {k: v / PMC_FRAMES for k, v in dur.items()}, None
+        return dur, None
     finally:
         shutil.rmtree(out, ignore_errors=True)
+
+
+def parse_kernel_trace(paths, frames=PMC_FRAMES):
+    """ms per frame of every frame kernel in rocprofv3 kernel-trace CSVs (the --pmc-child's warm-up
+    frame dropped): summed over the profiled frames, divided by their count."""
+    dur = {}
+    for f in paths:
+        with open(f) as fh:
+            for r in _after_first_frame(list(csv.DictReader(fh)), "Start_Timestamp"):
+                k = _kernel_base(r["Kernel_Name"])
+                if k in TRACE_KERNELS:
+                    dur[k] = dur.get(k, 0.0) + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+    return {k: v / frames for k, v in dur.items()}
+
+
+def kernel_sum_check(dur, hip_event_ms, tol=0.05):
+    """The per-kernel table must account for the frame: the rocprof kernel times summed per frame
+    against the serial frame's kernels timed with HIP events on their stream (gaps between launches
+    make the events' time the larger).  ok: within tol."""
+    if not dur or not hip_event_ms:
+        return None
+    s = sum(dur.values())
+    return dict(kernel_ms_rocprof_sum=round(s, 4), hip_event_ms=round(hip_event_ms, 4),
+                ratio=round(s / hip_event_ms, 4), ok=abs(s / hip_event_ms - 1) <= tol, tol=tol)
 
 
 def pmc_counters(args, deadline, cap_s=60.0, reserve_s=0.0):
@@ -462,9 +494,9 @@ def kernel_rooflines(dur, pmc, counters):
     # on segmented levels, §5.10): the two passes' algorithmic bytes are one pool, shared by their
     # kernels in proportion to time
     pass_of, pass_bytes = dict(KERNEL_PASS), dict(PASS_BYTES)
-    if "k_walk_first" in dur or "k_seg" in dur:
+    if "k_walk_first" in dur or "k_seg" in dur or "k_level" in dur:
         pass_of = {k: ("walk+first" if p in ("walk", "first") else p) for k, p in pass_of.items()}
-        pass_of["k_walk_first"] = pass_of["k_seg"] = "walk+first"
+        pass_of["k_walk_first"] = pass_of["k_seg"] = pass_of["k_level"] = "walk+first"
         pass_bytes["walk+first"] = dict(PASS_BYTES["walk"], **PASS_BYTES["first"])
     for k, ms in sorted(dur.items(), key=lambda kv: -kv[1]):
         c = pmc.get(k, {})
@@ -510,7 +542,28 @@ def kernel_rooflines(dur, pmc, counters):
     return out
 
 
-def hbm_8d(tot, s_per_frame, hbm_counted):
+INFINITY_CACHE_BYTES = 256 << 20     # MI355X last-level (Infinity / MALL) cache
+
+
+def scene_device_bytes(scene, lights=False):
+    """Device bytes of the resident scene (rt_internal.h layout): per node the 128-B walk record, the
+    parent link (8), node_ent (16) and node_dfs (4); per list entry the 80-B prim record, list_entity
+    (4), list_prefix (16) and within (4); the cull hierarchies (2c - 1 records of 32 B per node of c
+    entities); per entity its substance (4); the shade table; with lights the shadow tree (32 B per
+    node).  `walk_set` is what the walk and the entity tests read: node records, prims, cull boxes."""
+    n = int(scene.n_nodes)
+    cnt = np.asarray(scene.node_ent_count)
+    m, with_ents = int(cnt.sum()), int((cnt > 0).sum())
+    bvh = 2 * m - with_ents
+    walk = 128 * n + 80 * m + 32 * bvh
+    total = walk + (8 + 16 + 4) * n + (4 + 16 + 4) * m + 4 * len(scene.ent_type) + 48 * len(scene.shades)
+    if lights:
+        total += 32 * n
+        walk += 32 * n
+    return dict(total=int(total), walk_set=int(walk))
+
+
+def hbm_8d(tot, s_per_frame, hbm_counted, scene_bytes=None):
     """SURVEY §8(d)'s HBM roofline frame, with why it does not apply: the reference-equivalent bytes
     (what the reference's Set-order loop would read) and the kernels' own algorithmic bytes per frame,
     each over the frame time, against 8 TB/s, beside the HBM bytes the counters saw.  The scene (26 MB
@@ -526,7 +579,21 @@ def hbm_8d(tot, s_per_frame, hbm_counted):
                 kernel_alg_frac_of_peak=round(alg_b / s_per_frame / 1e9 / HBM_PEAK_GBS, 2),
                 hbm_bytes_counted_per_frame=int(hbm_counted),
                 hbm_counted_frac_of_peak=round(hbm_counted / s_per_frame / 1e9 / HBM_PEAK_GBS, 4),
-                note="not the binding roof: cache-resident scene and culled entity tests; see roofline.kernels")
+                scene_device_bytes=scene_bytes,
+                note=hbm_8d_note(scene_bytes))
+
+
+def hbm_8d_note(scene_bytes):
+    """Why §8(d)'s frame does not bind, from the scene's size against the 256 MiB Infinity Cache."""
+    if not scene_bytes:
+        return "culled entity tests; see roofline.kernels"
+    ws = scene_bytes["walk_set"]
+    if ws <= INFINITY_CACHE_BYTES:
+        return ("not the binding roof: the scene's walk / test working set (%.1f MB) fits the 256 MiB Infinity "
+                "Cache, and culling replaces the reference's exact tests; see roofline.kernels" % (ws / 1e6))
+    return ("the scene's walk / test working set (%.1f MB) exceeds the 256 MiB Infinity Cache: node and record "
+            "misses reach HBM (hbm_bytes_counted_per_frame), at latency rather than bandwidth; culling replaces "
+            "the reference's exact tests; see roofline.kernels" % (ws / 1e6))
 
 
 def exposure_bench(ctx, frame, stream, reps=20):
@@ -964,8 +1031,9 @@ def report(args, res, spec, scene, W, H, refmax, build_s, deadline, reporter):
             kr = kernel_rooflines(dur, pmc, tot)
             roofline["kernels"] = kr
             roofline["kernel_ms_rocprof_sum"] = round(sum(dur.values()), 4)
+            roofline["kernel_sum_check"] = kernel_sum_check(dur, res["kernel_ms"])
             hbm_counted = sum(v.get("hbm_bytes", 0) for v in kr.values())
-            roofline["hbm_8d"] = hbm_8d(tot, el / steps, hbm_counted)
+            roofline["hbm_8d"] = hbm_8d(tot, el / steps, hbm_counted, scene_device_bytes(scene, bool(LIGHTS_ON)))
             top = max(kr, key=lambda k: kr[k]["ms_per_frame"])
             t = kr[top]
             if "valu_issue_frac" in t or "hbm_frac" in t:

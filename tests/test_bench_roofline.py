@@ -5,6 +5,7 @@ applicable with its ratios to peak."""
 import os
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -80,3 +81,59 @@ def test_lights_option_reaches_every_context_and_the_profiled_child():
         assert cmd[cmd.index("--lights") + 1] == "0"
     finally:
         bench.LIGHTS_ON[:] = saved
+
+
+def _trace_csv(path, frames):
+    """A rocprofv3 kernel-trace CSV: a warm-up frame, then `frames` frames of the config-3 kernel set
+    with a bounce level as k_level and two lights' shadow passes (ns timestamps)."""
+    per_frame = [("k_frame_start", 34_000), ("k_walk_first<4, 64>", 2_120_000), ("k_shade<3>", 21_000),
+                 ("k_level<2>", 220_000), ("k_cont<3>", 10_000), ("k_shadow_walk<4>", 400_000),
+                 ("k_shadow_first<4>", 300_000), ("k_shadow_walk<4>", 410_000), ("k_shadow_first<4>", 290_000),
+                 ("k_shadow<8>", 26_000)]
+    t = 1_000_000
+    with open(path, "w") as fh:
+        fh.write("Kernel_Name,Start_Timestamp,End_Timestamp\n")
+        for f in range(frames + 1):
+            for name, ns in per_frame:
+                dur = ns * (3 if f == 0 else 1)          # the warm-up frame is slower: must be dropped
+                fh.write('"void (anonymous namespace)::%s(RtLaunch)",%d,%d\n' % (name, t, t + dur))
+                t += dur + 5_000
+
+
+def test_kernel_table_covers_every_frame_kernel(tmp_path):
+    """k_level and the shadow passes were missing from the per-kernel table.  The
+    trace kernels are now every __global__ of rt_kernels.hip, and the canned trace's per-frame times
+    come back for each of them, warm-up frame dropped, with the sum equal to the frame's kernels."""
+    for k in ("k_level", "k_shadow_walk", "k_shadow_first", "k_shadow", "k_walk_first", "k_seg", "k_cont",
+              "k_walk_refill", "k_frame_start"):
+        assert k in bench.TRACE_KERNELS, k
+    assert "k_debug_walk" not in bench.TRACE_KERNELS
+    p = tmp_path / "kt.csv"
+    _trace_csv(str(p), bench.PMC_FRAMES)
+    dur = bench.parse_kernel_trace([str(p)])
+    assert dur["k_level"] == pytest.approx(0.220)
+    assert dur["k_shadow_walk"] == pytest.approx(0.810) and dur["k_shadow_first"] == pytest.approx(0.590)
+    assert dur["k_shadow"] == pytest.approx(0.026) and dur["k_walk_first"] == pytest.approx(2.120)
+    total = sum(dur.values())
+    assert total == pytest.approx(3.831)
+    chk = bench.kernel_sum_check(dur, 3.90)
+    assert chk["ok"] and chk["ratio"] == pytest.approx(total / 3.90, rel=1e-3)
+    assert not bench.kernel_sum_check({"k_walk_first": 2.12}, 2.41)["ok"]     # k_level left out: -12 %
+
+
+def test_hbm_note_follows_the_scene_size():
+    """hbm_8d's note is computed from the scene's device bytes against the 256 MiB Infinity Cache
+    (config 3 fits, config 5 does not), not a fixed string."""
+    class Sc:
+        def __init__(self, n, ents_per_node, nodes_with):
+            self.n_nodes = n
+            self.node_ent_count = np.zeros(n, np.int32)
+            self.node_ent_count[:nodes_with] = ents_per_node
+            self.ent_type = np.zeros(nodes_with * ents_per_node, np.int32)
+            self.shades = np.zeros(10)
+    small = bench.scene_device_bytes(Sc(182_217, 1, 101_001))
+    big = bench.scene_device_bytes(Sc(2_350_000, 1, 1_001_001))
+    assert small["walk_set"] < bench.INFINITY_CACHE_BYTES < big["walk_set"]
+    assert "fits" in bench.hbm_8d_note(small) and "exceeds" in bench.hbm_8d_note(big)
+    h = bench.hbm_8d(TOT, 43e-3, 14.9e9, big)
+    assert "exceeds" in h["note"] and h["scene_device_bytes"]["walk_set"] == big["walk_set"]
