@@ -303,21 +303,22 @@ int  rt_frame_fault(rt_ctx *ctx, int32_t *fault);
 
 /* Shadow rays: a BUILD EXTENSION, off by default (the reference samples no lights,
  * src/raytracer.ts:168-277; BASELINE config 5 names "shadow rays").  Frozen definition (DESIGN.md
- * §3.6; the oracle's orc_set_lights implements the same): with n > 0 point lights, a ray that ends on
- * a matte surface (REFLECTION, not a mirror, not a light), after alter_ray and the path-length update,
- * at point p with the hit normal nrm and path length `path`, multiplies its colour channel-wise by
+ * §3.6, round 5; the oracle's orc_set_lights implements the same): with n > 0 point lights, a ray that
+ * ends on a matte surface (REFLECTION, not a mirror, not a light), after alter_ray and the path-length
+ * update, at point p with the hit normal nrm and path length `path`, multiplies its colour
+ * channel-wise by
  *     s = ambient + sum over lights l (in order) of  rgb_l * (cosine * isl)
  * where, in binary64 without contraction and in this order: v = pos_l - p; dist = sqrt(v.v) (skip the
  * light unless dist > 0); u = v * (1/dist); cosine = nrm.u (skip unless cosine > 0); the shadow ray
- * starts at q = p + u*1e-3 (move_slightly_forward), is seated like a continuation
- * (set_pos_and_dir without a node) and walked in the reference's walker order, each node's Set in
- * order; its FIRST hit decides: the light is blocked when that hit's entity is not a light and
- * |hit - q| < dist - 1e-3, or when the seat or the walk throws or reaches the step cap; otherwise
- * t = (path + dist) * distance_attenuation_factor and isl = 1/(EPSILON + t*t) (the reference's
- * inverse-square law, src/raytracer.ts:274-275).  Shadow-ray tests are not counted in rt_stats, and
- * hit ids / status stay those of the primary ray.  n = 0 (the default) restores the reference's
- * behaviour bit for bit.  Applies to the context's later frames (a changed list waits for the
- * context's frame in flight). */
+ * starts at q = p + u*1e-3 (move_slightly_forward).  The light is BLOCKED when some entity of the
+ * scene (held by a node's EntitySet) that is not a light has a collision_info(q, u) that hits, or
+ * throws, at a point h with sqrt((h-q).(h-q)) < dist - 1e-3: an existence question, whatever the
+ * order entities are tested in.  Otherwise t = (path + dist) * distance_attenuation_factor and
+ * isl = 1/(EPSILON + t*t) (the reference's inverse-square law, src/raytracer.ts:274-275).  Shadow-ray
+ * tests are not counted in rt_stats, and hit ids / status stay those of the primary ray.  n = 0 (the
+ * default) restores the reference's behaviour bit for bit.  Applies to the context's later frames (a
+ * changed list waits for the context's frame in flight); the first frame with lights after a scene
+ * change builds the GPU's search tree for it (synchronising that GPU's streams of this context). */
 #define RT_MAX_LIGHTS 4
 typedef struct rt_light {
     double pos[3];

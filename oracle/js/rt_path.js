@@ -400,26 +400,81 @@ const ST_OK = 0, ST_WARN = 1, ST_FAULT = 2;
 
 // ---- shadow rays: a BUILD EXTENSION the reference does not have (include/rt.h rt_set_lights,
 // DESIGN.md §3.6), restated on this object model from the frozen definition: manifest.lights /
-// manifest.ambient.  The C oracle's shadow_factor is the same definition.
-function shadow_blocked(sc, q, u, dist) {
-  const walker = sc.shadow_walker || (sc.shadow_walker = new OctreeWalker(sc.root));
-  try {
-    walker.set_pos_and_dir(q, u);
-    for (;;) {
-      const stop = walker.next();
-      if (stop === undefined) return false;
-      let hit, ent;
-      for (const e of stop.node.value) {
-        const c = e.collision_info({ start: q, dir: u });
-        if (c !== undefined) { hit = c; ent = e; break; }
-      }
-      if (hit === undefined) continue;
-      if (sc.m.shades[ent.shade].light) return false;
-      return vector.length(vector.sub(hit.point, q)) < dist - 1e-3;
-    }
-  } catch (e) {
-    return true;                                     // a throw blocks the light
+// manifest.ambient.  The C oracle's shadow_factor is the same definition.  The light is blocked when
+// some entity of the tree that is not a light has a forward hit (or a throwing test) nearer than
+// dist - 1e-3: an existence question, answered here by a descent that skips the subtrees whose
+// entities' geometry bounds the segment cannot meet.
+function geom_bounds(e) {                          // the collision geometry's bounds (not get_aabb)
+  let lo, hi;
+  if (e instanceof FaceEntity) {
+    lo = [0, 1, 2].map((i) => Math.min(e.v0.v[i], e.v1.v[i], e.v2.v[i]));
+    hi = [0, 1, 2].map((i) => Math.max(e.v0.v[i], e.v1.v[i], e.v2.v[i]));
+  } else {
+    const h = Math.abs(e instanceof SphereEntity ? e.diameter : e.size) * 0.5;
+    lo = e.pos.v.map((x) => x - h);
+    hi = e.pos.v.map((x) => x + h);
   }
+  if (!lo.concat(hi).every(Number.isFinite)) return { lo: [-Infinity, -Infinity, -Infinity], hi: [Infinity, Infinity, Infinity] };
+  return { lo, hi };
+}
+
+function subtree_bounds(t) {                       // cached on the node: { lo, hi, n }
+  if (t.sb) return t.sb;
+  const sb = { lo: [Infinity, Infinity, Infinity], hi: [-Infinity, -Infinity, -Infinity], n: t.value.size };
+  const grow = (b) => { for (let i = 0; i < 3; i++) { sb.lo[i] = Math.min(sb.lo[i], b.lo[i]); sb.hi[i] = Math.max(sb.hi[i], b.hi[i]); } };
+  for (const e of t.value) grow(e.sb || (e.sb = geom_bounds(e)));
+  for (const c of t.children) {
+    if (c === undefined) continue;
+    const cb = subtree_bounds(c);
+    if (cb.n) { sb.n += cb.n; grow(cb); }
+  }
+  return (t.sb = sb);
+}
+
+function seg_may_meet(q, u, dist, b) {             // conservative slab test (oracle seg_may_meet)
+  let S = 1 + Math.abs(dist);
+  for (let i = 0; i < 3; i++) {
+    S = Math.max(S, Math.abs(q.v[i]));
+    if (Number.isFinite(b.lo[i])) S = Math.max(S, Math.abs(b.lo[i]));
+    if (Number.isFinite(b.hi[i])) S = Math.max(S, Math.abs(b.hi[i]));
+  }
+  const m = S * Math.pow(2, -20);
+  let t0 = -m, t1 = dist + m;
+  for (let i = 0; i < 3; i++) {
+    const l = b.lo[i] - m, h = b.hi[i] + m;
+    if (u.v[i] === 0) { if (q.v[i] < l || q.v[i] > h) return false; continue; }
+    let a = (l - q.v[i]) / u.v[i], c = (h - q.v[i]) / u.v[i];
+    if (a > c) { const x = a; a = c; c = x; }
+    if (a > t0) t0 = a;
+    if (c < t1) t1 = c;
+    if (t0 > t1) return false;
+  }
+  return true;
+}
+
+function entity_blocks(sc, e, q, u, lim) {
+  let hit;
+  try {
+    hit = e.collision_info({ start: q, dir: u });
+  } catch (err) {                                  // a throwing test: its hit point decides
+    hit = { point: intersection_point({ start: q, dir: u }, select_forward(e.box_math.line_intersection({ start: q, dir: u }))[0]) };
+  }
+  if (hit === undefined || sc.m.shades[e.shade].light) return false;
+  return vector.length(vector.sub(hit.point, q)) < lim;
+}
+
+function subtree_blocks(sc, t, q, u, dist, lim) {
+  const sb = subtree_bounds(t);
+  if (!sb.n || !seg_may_meet(q, u, dist, sb)) return false;
+  for (const e of t.value) {
+    if (seg_may_meet(q, u, dist, e.sb) && entity_blocks(sc, e, q, u, lim)) return true;
+  }
+  for (const c of t.children) if (c !== undefined && subtree_blocks(sc, c, q, u, dist, lim)) return true;
+  return false;
+}
+
+function shadow_blocked(sc, q, u, dist) {
+  return subtree_blocks(sc, sc.root, q, u, dist, dist - 1e-3);
 }
 
 function shadow_factor(sc, p, nrm, path_len) {

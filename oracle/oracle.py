@@ -52,6 +52,9 @@ def lib():
     L.orc_walker_next.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_int)]
     L.orc_set_tables.argtypes = [vp, C.POINTER(abi.rt_shade), i, pd, i]
     L.orc_set_lights.argtypes = [vp, C.POINTER(abi.rt_light), i, C.c_double]
+    L.orc_set_shadow_brute.argtypes = [vp, i]
+    L.orc_set_shadow_brute.restype = None
+    L.orc_shadow_blocked.argtypes = [vp, vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_double]
     L.orc_add_entity.argtypes = [vp, vp, i, pd, i, i, i, i, C.POINTER(vp)]
     L.orc_entity_in_set.argtypes = [vp, i]
     L.orc_entity_at_pos.argtypes = [vp, vp, pd]
@@ -181,6 +184,15 @@ class World:
         r = self.L.orc_set_lights(self.h, arr, len(lights), float(ambient))
         if r != 0:
             raise ValueError("orc_set_lights: %d" % r)
+
+    def set_shadow_brute(self, on=True):
+        """Shadow rays: test every entity of the tree instead of the bounded search (the two must agree:
+        the bounds only skip entities whose test cannot block)."""
+        self.L.orc_set_shadow_brute(self.h, 1 if on else 0)
+
+    def shadow_blocked(self, root, q, u, dist):
+        """One shadow ray (include/rt.h rt_set_lights): blocked before a light at distance dist?"""
+        return bool(self.L.orc_shadow_blocked(self.h, root, _vec(q), _vec(u), float(dist)))
 
     def set_images(self, images):
         """ImageTextures, [H, W, 3] uint8 each (copied by the oracle)."""

@@ -77,6 +77,10 @@ struct onode {
     int set_n, set_cap;
     int dfs_id;
     onode *next_alloc;
+    /* shadow rays (build extension): the geometry bounds of every entity at or below this node, and
+     * their count (0: none); filled by shadow_bounds before a frame with lights */
+    double sb_lo[3], sb_hi[3];
+    int64_t sb_n;
 };
 
 typedef struct oentity {
@@ -118,6 +122,7 @@ struct oworld {
     int n_lights;            /* shadow rays (build extension, orc_set_lights): 0 = the reference */
     double ambient;
     rt_light lights[RT_MAX_LIGHTS];
+    int shadow_brute;        /* orc_set_shadow_brute: test every entity (pins the bounded search) */
 };
 
 oworld *orc_world_new(void)
@@ -1223,38 +1228,141 @@ int orc_set_lights(oworld *w, const rt_light *lights, int n, double ambient)
     return 0;
 }
 
-/* 1 when the shadow ray (q, u) is blocked before dist: its first hit in walk order (Set order within
- * a node) decides; a throw or the step cap blocks.  wks: a walker whose counters nobody reads. */
-static int shadow_blocked(oworld *w, owalker *wks, const double q[3], const double u[3], double dist)
+void orc_set_shadow_brute(oworld *w, int on) { w->shadow_brute = on != 0; }
+
+/* The bounds of an entity's collision geometry (not Entity.get_aabb): sphere centre +- |d|/2, box
+ * centre +- |size|/2 (intersection.Box is centred, src/entities/entity_box.ts:54-56), triangle the
+ * vertices' min / max.  Non-finite geometry gets an unbounded box. */
+static void geom_bounds(const oentity *e, double lo[3], double hi[3])
 {
-    if (orc_walker_set(wks, q, u, NULL, 0) < 0) return 1;
-    for (;;) {
-        onode *node, *pt;
-        int po;
-        int r = orc_walker_next(wks, &node, &pt, &po);
-        if (r < 0) return 1;
-        if (r == 0) return 0;
-        int hit_id = -1;
-        ohit h;
-        for (int i = 0; i < node->set_n; i++) {
-            const oentity *e = &w->ents[node->set[i]];
-            memset(&h, 0, sizeof h);
-            int got;
-            if (e->type == RT_ENT_SPHERE) got = sphere_collision(e, q, u, &h);
-            else if (e->type == RT_ENT_BOX) got = box_collision(e, q, u, &h);
-            else got = face_collision(e, q, u, &h);
-            if (got) { hit_id = node->set[i]; break; }
+    const double *g = e->g;
+    int finite = 1;
+    for (int i = 0; i < 3; i++) {
+        if (e->type == RT_ENT_FACE) {
+            lo[i] = g[i]; hi[i] = g[i];
+            for (int v = 1; v < 3; v++) {
+                if (g[3 * v + i] < lo[i]) lo[i] = g[3 * v + i];
+                if (g[3 * v + i] > hi[i]) hi[i] = g[3 * v + i];
+            }
+            for (int v = 0; v < 3; v++) finite = finite && isfinite(g[3 * v + i]);
+        } else {
+            double h = fabs(g[3]) * 0.5;
+            lo[i] = g[i] - h; hi[i] = g[i] + h;
+            finite = finite && isfinite(lo[i]) && isfinite(hi[i]);
         }
-        if (hit_id < 0) continue;
-        if (h.fault) return 1;
-        if (w->shades[w->ents[hit_id].shade].light) return 0;
-        double diff[3] = {h.point[0] - q[0], h.point[1] - q[1], h.point[2] - q[2]};
-        return sqrt(vdot(diff, diff)) < dist - 1e-3;
+    }
+    if (!finite)
+        for (int i = 0; i < 3; i++) { lo[i] = -INFINITY; hi[i] = INFINITY; }
+}
+
+/* Post-order: every node's sb_lo / sb_hi / sb_n over its own set and its subtrees. */
+static void shadow_bounds(oworld *w, onode *t)
+{
+    for (int i = 0; i < 3; i++) { t->sb_lo[i] = INFINITY; t->sb_hi[i] = -INFINITY; }
+    t->sb_n = t->set_n;
+    for (int k = 0; k < t->set_n; k++) {
+        double lo[3], hi[3];
+        geom_bounds(&w->ents[t->set[k]], lo, hi);
+        for (int i = 0; i < 3; i++) {
+            if (lo[i] < t->sb_lo[i]) t->sb_lo[i] = lo[i];
+            if (hi[i] > t->sb_hi[i]) t->sb_hi[i] = hi[i];
+        }
+    }
+    for (int c = 0; c < 8; c++) {
+        onode *ch = t->child[c];
+        if (!ch) continue;
+        shadow_bounds(w, ch);
+        if (!ch->sb_n) continue;
+        t->sb_n += ch->sb_n;
+        for (int i = 0; i < 3; i++) {
+            if (ch->sb_lo[i] < t->sb_lo[i]) t->sb_lo[i] = ch->sb_lo[i];
+            if (ch->sb_hi[i] > t->sb_hi[i]) t->sb_hi[i] = ch->sb_hi[i];
+        }
     }
 }
 
+/* Whether the segment q + u t, t in [0, dist], may meet the box [lo, hi]: a slab test on the box
+ * widened by 2^-20 of the largest magnitude involved (and by as much on the parameter), so that a
+ * hit point computed in binary64 on the segment's part before dist is never pruned.  Conservative
+ * only: the decision itself is the exact test of each entity that passes. */
+static int seg_may_meet(const double q[3], const double u[3], double dist, const double lo[3], const double hi[3])
+{
+    double S = 1 + fabs(dist);
+    for (int i = 0; i < 3; i++) {
+        if (fabs(q[i]) > S) S = fabs(q[i]);
+        if (isfinite(lo[i]) && fabs(lo[i]) > S) S = fabs(lo[i]);
+        if (isfinite(hi[i]) && fabs(hi[i]) > S) S = fabs(hi[i]);
+    }
+    const double m = S * 0x1p-20;
+    double t0 = -m, t1 = dist + m;
+    for (int i = 0; i < 3; i++) {
+        const double l = lo[i] - m, h = hi[i] + m;
+        if (u[i] == 0) {
+            if (q[i] < l || q[i] > h) return 0;
+            continue;
+        }
+        double a = (l - q[i]) / u[i], b = (h - q[i]) / u[i];
+        if (a > b) { double x = a; a = b; b = x; }
+        if (a > t0) t0 = a;                                   /* a NaN bound never prunes */
+        if (b < t1) t1 = b;
+        if (t0 > t1) return 0;
+    }
+    return 1;
+}
+
+/* Whether entity e blocks the shadow ray: not a light, and its collision_info(q, u) hits (or throws,
+ * with the hit point it computed) at h with |h - q| < lim. */
+static int entity_blocks(const oworld *w, const oentity *e, const double q[3], const double u[3], double lim)
+{
+    ohit h;
+    memset(&h, 0, sizeof h);
+    int got;
+    if (e->type == RT_ENT_SPHERE) got = sphere_collision(e, q, u, &h);
+    else if (e->type == RT_ENT_BOX) got = box_collision(e, q, u, &h);
+    else got = face_collision(e, q, u, &h);
+    if (!got || w->shades[e->shade].light) return 0;
+    double diff[3] = {h.point[0] - q[0], h.point[1] - q[1], h.point[2] - q[2]};
+    return sqrt(vdot(diff, diff)) < lim;
+}
+
+static int subtree_blocks(const oworld *w, const onode *t, const double q[3], const double u[3], double dist,
+                          double lim)
+{
+    const int brute = w->shadow_brute;
+    if (!t->sb_n || (!brute && !seg_may_meet(q, u, dist, t->sb_lo, t->sb_hi))) return 0;
+    for (int k = 0; k < t->set_n; k++) {
+        const oentity *e = &w->ents[t->set[k]];
+        if (!brute) {
+            double lo[3], hi[3];
+            geom_bounds(e, lo, hi);
+            if (!seg_may_meet(q, u, dist, lo, hi)) continue;
+        }
+        if (entity_blocks(w, e, q, u, lim)) return 1;
+    }
+    for (int c = 0; c < 8; c++)
+        if (t->child[c] && subtree_blocks(w, t->child[c], q, u, dist, lim)) return 1;
+    return 0;
+}
+
+/* 1 when the shadow ray (q, u) toward a light at distance dist (from the hit point) is blocked: some
+ * entity of the tree that is not a light has a forward hit, or a throwing test, nearer than
+ * dist - 1e-3 (include/rt.h rt_set_lights).  An existence question: the order entities are visited in
+ * does not matter, and the bounds only skip entities whose test cannot report such a hit
+ * (shadow_brute tests them all).  Needs shadow_bounds(root) first. */
+static int shadow_blocked(oworld *w, onode *root, const double q[3], const double u[3], double dist)
+{
+    return subtree_blocks(w, root, q, u, dist, dist - 1e-3);
+}
+
+/* test hook: one shadow ray's answer on the tree as it is now (bounds recomputed) */
+int orc_shadow_blocked(oworld *w, onode *root, const double q[3], const double u[3], double dist)
+{
+    shadow_bounds(w, root);
+    return shadow_blocked(w, root, q, u, dist);
+}
+
 /* the matte hit's light factor: ambient + the unblocked lights' rgb * (cosine * isl) */
-static void shadow_factor(oworld *w, owalker *wks, const rt_config_desc *cfg, const double p[3],
+static void shadow_factor(oworld *w, onode *root, const rt_config_desc *cfg, const double p[3],
                           const double nrm[3], double path, double s[3])
 {
     s[0] = s[1] = s[2] = w->ambient;
@@ -1268,7 +1376,7 @@ static void shadow_factor(oworld *w, owalker *wks, const rt_config_desc *cfg, co
         double cosine = vdot(nrm, u);
         if (!(cosine > 0)) continue;
         double q[3] = {p[0] + u[0] * 1e-3, p[1] + u[1] * 1e-3, p[2] + u[2] * 1e-3};
-        if (shadow_blocked(w, wks, q, u, dist)) continue;
+        if (shadow_blocked(w, root, q, u, dist)) continue;
         double t = (path + dist) * cfg->distance_attenuation_factor;
         double isl = 1.0 / (2.220446049250313e-16 + t * t);
         double k = cosine * isl;
@@ -1276,8 +1384,7 @@ static void shadow_factor(oworld *w, owalker *wks, const rt_config_desc *cfg, co
     }
 }
 
-static void trace_ray(const trace_ctx *tc, owalker *wk, owalker *wks, const double dir0[3], uint64_t pixel,
-                      ray_out *ro)
+static void trace_ray(const trace_ctx *tc, owalker *wk, const double dir0[3], uint64_t pixel, ray_out *ro)
 {
     int matte = 0;                                                           /* shadow rays */
     double mnrm[3] = {0, 0, 0};
@@ -1408,7 +1515,7 @@ static void trace_ray(const trace_ctx *tc, owalker *wk, owalker *wks, const doub
 out:
     if (matte) {
         double sf[3];
-        shadow_factor(w, wks, cfg, o, mnrm, path, sf);
+        shadow_factor(w, tc->root, cfg, o, mnrm, path, sf);
         for (int i = 0; i < 3; i++) col[i] = col[i] * sf[i];
     }
     ro->rgb[0] = col[0]; ro->rgb[1] = col[1]; ro->rgb[2] = col[2];
@@ -1426,7 +1533,7 @@ typedef struct frame_job {
     int32_t *hit_entity, *hit_node, *segs;
     uint8_t *status;
     int tid, nthreads;
-    owalker *wk, *wks;      /* wks: shadow rays' walker (its counters are not reported) */
+    owalker *wk;
     int64_t counters[11];
 } frame_job;
 
@@ -1439,7 +1546,7 @@ static void *frame_worker(void *arg)
         int p = j->pix ? j->pix[k] : k;
         ray_out ro;
         memset(&ro, 0, sizeof ro);
-        trace_ray(j->tc, j->wk, j->wks, j->dirs + 3 * (size_t)p, (uint64_t)p, &ro);
+        trace_ray(j->tc, j->wk, j->dirs + 3 * (size_t)p, (uint64_t)p, &ro);
         /* ExposureBuffer.set_color_i — src/view/exposure_buffer.ts:77-91 */
         float *px = j->rgb + 3 * (size_t)p;
         for (int c = 0; c < 3; c++) {
@@ -1494,6 +1601,7 @@ int orc_trace_frame(oworld *w, onode *root, const rt_camera_desc *cam, const rt_
     tc.start_tree = r == 1 ? st : NULL;
     tc.start_oct = so;
     tc.start_sub = se >= 0 ? w->ents[se].substance : cfg->default_substance;
+    if (w->n_lights) shadow_bounds(w, root);                    /* shadow rays: the tree's bounds */
 
     frame_job *jobs = (frame_job *)calloc((size_t)nthreads, sizeof(frame_job));
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
@@ -1503,7 +1611,6 @@ int orc_trace_frame(oworld *w, onode *root, const rt_camera_desc *cam, const rt_
         j->rgb = rgb_inout; j->hit_entity = hit_entity; j->hit_node = hit_node; j->segs = segments;
         j->status = status; j->tid = t; j->nthreads = nthreads;
         j->wk = orc_walker_new(w, root, 0);
-        j->wks = orc_walker_new(w, root, 0);
     }
     if (nthreads == 1) frame_worker(&jobs[0]);
     else {

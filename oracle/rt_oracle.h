@@ -60,6 +60,10 @@ int  orc_set_tables(oworld *w, const rt_shade *shades, int n_shades, const doubl
 int  orc_set_images(oworld *w, const rt_image_desc *images, int n);      /* ImageTextures (copied) */
 /* shadow rays, a build extension (include/rt.h rt_set_lights): n = 0 is the reference */
 int  orc_set_lights(oworld *w, const rt_light *lights, int n, double ambient);
+/* shadow rays: test every entity instead of the bounded search (tests pin the two equal) */
+void orc_set_shadow_brute(oworld *w, int on);
+/* test hook: whether the shadow ray from q along u toward a light at distance dist is blocked */
+int  orc_shadow_blocked(oworld *w, onode *root, const double q[3], const double u[3], double dist);
 double orc_atan(double x);                                                 /* Math.atan (V8 / fdlibm) */
 double orc_atan2(double y, double x);                                      /* Math.atan2 (V8 / fdlibm) */
 void orc_uv_map_sphere(const double d[3], double uv[2]);                  /* src/math/uv_mapping.ts:19-25 */

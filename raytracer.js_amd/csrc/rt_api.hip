@@ -82,8 +82,9 @@ struct RtDevice {
     hipStream_t stream = nullptr;
     RtDevScene scene{};
     DevBuf b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters,
-        b_fault, b_lights, b_shadow;
+        b_fault, b_lights, b_shadow, b_sh, b_sh_tmp, b_sh_ints;
     uint64_t lights_seq = 0;                     // the rt_set_lights call b_lights holds
+    uint64_t sh_epoch = 0;                       // the scene (store epoch) b_sh's shadow tree was built for
     std::vector<std::array<hipEvent_t, 2>> ev;   // trace-kernel timing ring
     int ev_next = 0, ev_count = 0;
     hipEvent_t sync = nullptr;                   // cross-stream / cross-device ordering
@@ -580,6 +581,34 @@ static int check_frame_args(rt_ctx *c, const rt_camera_desc *cam, const rt_confi
 // d.b_rgb / d.b_hit_* unless the caller repoints L.rgb.  Device d must be current.
 enum { WANT_IDS = 1, WANT_STATUS = 2 };
 
+// Shadow rays (rt_set_lights): the shadow tree of device d's scene (rt_launch_shadow_tree), built at the
+// first frame with lights after each upload, update or edit (d.scene is replaced by those, without
+// it).  Synchronises the device's streams first: a frame of this context still in flight on this GPU
+// may read the tree being rebuilt.
+static int ensure_shadow_tree(rt_ctx *c, RtDevice &d)
+{
+    const uint64_t ep = rt_store_epoch(c->store);
+    if (d.scene.shnode && d.sh_epoch == ep) return RT_OK;
+    int r;
+    if ((r = use_device(d)) != RT_OK) return r;
+    if (d.stream) HIP_TRY(hipStreamSynchronize(d.stream));
+    if (&d == &c->dev[0])
+        for (RtDevice &b : c->band)
+            if (b.stream) HIP_TRY(hipStreamSynchronize(b.stream));
+    const size_t N = (size_t)std::max(d.scene.n_nodes, 1);
+    if ((r = d.b_sh.ensure(sizeof(RtShNode) * N)) != RT_OK || (r = d.b_sh_tmp.ensure(sizeof(RtShNode) * N)) != RT_OK ||
+        (r = d.b_sh_ints.ensure(sizeof(int32_t) * (2 * N + 2))) != RT_OK)
+        return r;
+    int32_t n_sh = 0;
+    if ((r = rt_launch_shadow_tree(d.scene, (RtShNode *)d.b_sh_tmp.p, (RtShNode *)d.b_sh.p, (int32_t *)d.b_sh_ints.p,
+                                   d.stream, &n_sh)) != RT_OK)
+        return r;
+    d.scene.shnode = (const RtShNode *)d.b_sh.p;
+    d.scene.n_sh = n_sh;
+    d.sh_epoch = ep;
+    return RT_OK;
+}
+
 // The newest completed counter copy of device d into its snapshot (the grid hints and the host-frame
 // streaming gate read it).  A frame that took a buffer but sent no counters (fused small frame, empty
 // part, an error before the copy) never records its event, and the query then reports success: the
@@ -684,6 +713,13 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
         L.n_lights = c->n_lights;
         L.ambient = c->ambient;
         L.lights = (const rt_light *)d.b_lights.p;
+        // the shadow tree belongs to the GPU's scene: a band (dev[0]'s GPU) takes dev[0]'s
+        RtDevice &ph = (&d >= c->band && &d < c->band + RT_MAX_BANDS) ? c->dev[0] : d;
+        if ((r = ensure_shadow_tree(c, ph)) != RT_OK) return r;
+        if ((r = use_device(d)) != RT_OK) return r;
+        d.scene.shnode = ph.scene.shnode;
+        d.scene.n_sh = ph.scene.n_sh;
+        L.scene = d.scene;
     }
     if (c->split && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {
         // split path buffers: cand_cap node ids per pixel, k-major.  If they cannot

@@ -65,6 +65,19 @@ struct alignas(16) RtPrim {
 };
 static_assert(sizeof(RtPrim) == 80, "RtPrim must stay 80 bytes");
 
+// Shadow rays' search tree (rt_set_lights): the octree nodes whose subtree holds
+// entities, in DFS pre-order (children in octant order), each with the union of its subtree's cull
+// boxes (the cull hierarchies' root boxes: entity AABBs widened and rounded outward to f32) and the
+// record after its subtree.  A hit record goes on to the next one (its first child, or the record
+// after it), a missed one to `skip`: stackless.  Built on the device per scene (rt_launch_shadow_tree).
+struct alignas(16) RtShNode {
+    float lo[3];
+    int32_t skip;      // the record after this subtree (-1: the end)
+    float hi[3];
+    int32_t root;      // this node's own cull hierarchy (-1: no entities of its own)
+};
+static_assert(sizeof(RtShNode) == 32, "RtShNode must stay 32 bytes");
+
 // Per-node cull hierarchy: a binary BVH over one node's entity list, stored in
 // depth-first order with skip links (stackless).  Bounds are the entities' AABBs widened by a
 // margin and rounded outward to f32, so a ray that the exact binary64 test can report as hitting
@@ -93,6 +106,8 @@ struct RtDevScene {
     int32_t n_top;              // slots [0, n_top) hold the upper levels breadth-first (RT_TOP_LEVELS; else 0)
     int32_t bvh_leaf;           // cull-hierarchy leaves hold up to this many entities (a node with no more
                                 // entities is one leaf: its prims at node_ent.x in order)
+    const RtShNode *shnode;     // shadow rays' search tree, n_sh records (null until a frame with lights
+    int32_t n_sh;               // builds it: rt_api.hip ensure_shadow_tree)
 };
 
 // A ray of the split path at its first continuation (segment start after a mirror / transmission
@@ -118,10 +133,9 @@ static_assert(sizeof(RtLate) == 32, "RtLate must stay 32 bytes");
 // write_pixel writes.
 struct RtShadowRec {
     double p[3], n[3], col[3], path;
-    double s[3];                                // the light factor so far (ambient, then light by light)
     int32_t pix, hit_ent, hit_node, segments;
 };
-static_assert(sizeof(RtShadowRec) == 120, "RtShadowRec must stay 120 bytes");
+static_assert(sizeof(RtShadowRec) == 96, "RtShadowRec must stay 96 bytes");
 
 // Per-frame state computed on the device by the setup kernel.
 struct RtFrameSetup {
@@ -252,15 +266,12 @@ struct RtLaunch {
     double ambient;
     const rt_light *lights;
     RtShadowRec *shadow_q;                      // split path with lights: [rows*W] deferred matte ends
-                                                // (count ctr[2], claim head ctr[3]), else null
-    int32_t shadow_light;                       // the light of a k_shadow_walk / k_shadow_first launch
+                                                // (count ctr[2], k_shadow's claim head ctr[3]), else null
 };
 
-// ctr: [0] overflow count, [1] its claim head, [2] deferred matte ends (shadow rays), [3] their
-// write pass's head; a block of RT_CTR_LEVEL per bounce level from 4; then the shadow passes' claim
-// heads (walk and first-hit per light)
-enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_SHADOW = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1),
-       RT_CTR_INTS = RT_CTR_SHADOW + 16 };
+// ctr: [0] overflow count, [1] its claim head, [2] deferred matte ends (shadow rays), [3] k_shadow's
+// claim head; a block of RT_CTR_LEVEL per bounce level from 4
+enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };
 
 // walk_wait / walk_done (host-frame bands): the level-0 walk pass waits for event walk_wait (the
 // previous band's level-0 walk) and walk_done is recorded after it, so bands' walks run in order.
@@ -272,6 +283,10 @@ int rt_launch_exposure_stats(const float *d_rgb, long long n, double *d_partials
 int rt_launch_tonemap(const float *d_rgb, long long n, double low, double high, uint8_t *d_rgba, void *stream);
 int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[3], int include_undefined,
                          int max_out, int32_t *d_tree, int32_t *d_oct, int32_t *d_n, void *stream);
+// The shadow tree of scene S into out[0 .. *n_out) (tmp: S.n_nodes records, ints: 2 * S.n_nodes + 2
+// int32 of scratch).  Synchronises `stream` twice (the deepest level, the record count).
+int rt_launch_shadow_tree(const RtDevScene &S, RtShNode *tmp, RtShNode *out, int32_t *ints, void *stream,
+                          int32_t *n_out);
 
 // ---- multi-device frame assembly (rt_multi.hip) -------------------------------------------------------
 // Rows between a frame (H rows of row_bytes) and the stacked parts (n_parts x max_rows rows):

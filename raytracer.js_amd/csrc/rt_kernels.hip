@@ -1254,31 +1254,72 @@ __device__ __forceinline__ RtCont *lvl_queue(const RtLaunch &L, int k)
 }
 
 // ---- shadow rays (a build extension, rt_set_lights; definition: include/rt.h) ----
-// Whether the shadow ray from q along u (unit) reaches a light at distance dist: its first hit in the
-// reference's walk order decides.  The work is not counted (cs is the caller's scratch).
-__device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, const double q[3], const double u[3], double dist,
-                               Counters &cs)
+// A light is blocked when some entity of the scene that is not a light has a forward hit (or a
+// throwing test) nearer than dist - 1e-3 from the shadow ray's start: an existence question, so the
+// search may visit entities in any order and skip any it can prove cannot answer it.  It runs over the
+// shadow tree (RtShNode: the octree's non-empty subtrees in pre-order with their cull boxes' union),
+// then each visited node's own cull hierarchy, pruning boxes the segment [0, dist] misses, with the
+// exact binary64 test as the only decision: one flat loop (a trip is one tree record, one hierarchy
+// record or one exact test), like scan_first.
+
+// The slab test of ray_box on the segment t in [0, tlim] (tlim: the light's distance rounded up).
+__device__ __forceinline__ bool ray_box_seg(const float *lo, const float *hi, const RayBox &rb, float tlim)
 {
-    Walker w;
-    if (walker_set(S, w, q, u, false, 0, 0, cs) < 0) return true;          // the seat throws
+    const float tx0 = (lo[0] - rb.ox) * rb.ix, tx1 = (hi[0] - rb.ox) * rb.ix;
+    const float ty0 = (lo[1] - rb.oy) * rb.iy, ty1 = (hi[1] - rb.oy) * rb.iy;
+    const float tz0 = (lo[2] - rb.oz) * rb.iz, tz1 = (hi[2] - rb.oz) * rb.iz;
+    const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tlim));
+    return tmin <= tmax;
+}
+
+// Whether prim `slot` blocks: its collision_info hits (or throws, with the point it computed), it is
+// not a light, and |h - q| < lim.
+__device__ __forceinline__ bool prim_blocks(const RtDevScene &S, int slot, const double q[3], const double u[3],
+                                            double lim)
+{
+    const RtPrim &pr = S.prim[slot];
+    Hit h;
+    if (prim_hit(pr, q, u, h) == 0) return false;
+    if (S.shades[pr.meta >> 2].light) return false;
+    const double a = h.p[0] - q[0], b = h.p[1] - q[1], e = h.p[2] - q[2];
+    return sqrt(dot3(a, b, e, a, b, e)) < lim;
+}
+
+// The shadow ray from q along u (unit) toward a light at distance dist (from the hit point, q being
+// 1e-3 along u from it).  Culling off (or a ray the f32 boxes cannot serve: rb.ok) tests every entity.
+// Why the pruning is exact: a blocking hit lies within its entity's widened box at a parameter below
+// dist - 1e-3 (|u| = 1 to an ulp), and the f32 slab test errs far less than the widening (§5.1), so
+// its box, and every enclosing union, passes the segment test up to tlim >= dist.
+__device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, const double q[3], const double u[3],
+                                            double dist)
+{
     const RayBox rb = make_raybox(q, u);
+    const bool prune = cull && rb.ok;
+    float tlim = (float)(dist * 1.0001);
+    if (!(tlim >= 0.0f)) tlim = INFINITY;
+    const double lim = dist - 1e-3;
+    int k = S.n_sh > 0 ? 0 : -1, i = -1, slot = 0, end = 0;
     for (;;) {
-        int node, pt, po;
-        const int r = walker_next<false>(S, w, node, pt, po, cs);
-        if (r < 0) return true;                                             // throw, step cap
-        if (r == 0) return false;
-        const int4 ent = reinterpret_cast<const int4 *>(S.node_ent)[node];
-        if (ent.y == 0) continue;
-        Hit h;
-        int rank;
-        long long box = 0;
-        const int hk = node_first_hit<false>(S, ent, q, u, rb, cull, cs, box, h, rank);
-        if (hk < 0) continue;
-        const RtPrim &pr = S.prim[hk];
-        if (prim_hit(pr, q, u, h) < 0) return true;                         // the winner throws
-        if (S.shades[pr.meta >> 2].light) return false;
-        const double a = h.p[0] - q[0], b = h.p[1] - q[1], e = h.p[2] - q[2];
-        return sqrt(dot3(a, b, e, a, b, e)) < dist - 1e-3;
+        if (slot < end) {
+            if (prim_blocks(S, slot, q, u, lim)) return true;
+            slot++;
+        } else if (i >= 0) {
+            const RtBvh b = S.bvh[i];
+            if (prune && !ray_box_seg(b.lo, b.hi, rb, tlim)) i = b.skip;
+            else if (b.info < 0) i++;
+            else { slot = b.info >> 4; end = slot + (b.info & 15); i = b.skip; }
+        } else if (k >= 0) {
+            const RtShNode t = S.shnode[k];
+            if (!prune || ray_box_seg(t.lo, t.hi, rb, tlim)) {
+                i = t.root;                                  // its own entities, then its subtree
+                k = k + 1 < S.n_sh ? k + 1 : -1;
+            } else {
+                k = t.skip;
+            }
+        } else {
+            return false;
+        }
     }
 }
 
@@ -1311,17 +1352,16 @@ __device__ __forceinline__ void shadow_add(const RtLaunch &L, const rt_light &lt
 }
 
 // The matte hit's light factor s (per channel): ambient + the unblocked lights' rgb * cosine * isl
-// (the fused kernels; the split path runs the same steps as k_shadow_walk / k_shadow_first passes).
+// (the fused kernels inline; the split path's k_shadow per deferred record).
 __device__ __forceinline__ void shadow_factor(const RtDevScene &S, const RtLaunch &L, bool cull, const double p[3],
                                               const double nrm[3], double path, double s[3])
 {
-    Counters cs = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     s[0] = s[1] = s[2] = L.ambient;
     for (int l = 0; l < L.n_lights; l++) {
         const rt_light lt = L.lights[l];
         double q[3], u[3], dist, cosine;
         if (!shadow_ray(lt, p, nrm, q, u, dist, cosine)) continue;
-        if (shadow_blocked(S, cull, q, u, dist, cs)) continue;
+        if (shadow_blocked(S, cull, q, u, dist)) continue;
         shadow_add(L, lt, path, dist, cosine, s);
     }
 }
@@ -1336,7 +1376,6 @@ __device__ __forceinline__ void shadow_push(const RtLaunch &L, const double p[3]
     e.n[0] = n[0]; e.n[1] = n[1]; e.n[2] = n[2];
     e.col[0] = col0; e.col[1] = col1; e.col[2] = col2;
     e.path = path;
-    e.s[0] = e.s[1] = e.s[2] = L.ambient;
     e.pix = pix;
     e.hit_ent = R.hit_ent;
     e.hit_node = R.hit_node;
@@ -2338,123 +2377,100 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
 }
 
 // Shadow rays on the split path (rt_set_lights): the matte ends the frame's passes
-// deferred (L.shadow_q, count ctr[2]) get their light factor as a walk pass and a first-hit pass per
-// light, the split path's own machinery (walk_item: the candidate lists of the shadow ray, seated
-// like a continuation; scan_first: the first candidate with an exact hit), then k_shadow writes the
-// pixels.  The first hit decides as shadow_blocked does: a hit found in the list decides by its
-// distance (or, on a light, lets the light through); no hit blocks only after a throw or the step
-// cap (cand_n's end status); an overflowed list runs shadow_blocked itself.  Record q's lists use
-// slot q of the frame's candidate buffers, free once k_cont is done.
-constexpr int32_t SHADOW_NO_RAY = -2;             // cand_n: this light is skipped for the record
-
-// Record q's shadow ray toward lt after its walk (cn = its cand_n): the first hit in its list decides,
-// and an unblocked light's term is added to the record's factor.
-__device__ __forceinline__ void shadow_decide(const RtLaunch &L, const RtDevScene &S, bool cull, const rt_light &lt,
-                                              RtShadowRec &e, const double o[3], const double d[3], double dist,
-                                              double cosine, int cn, uint32_t stride, uint32_t q, Counters &c)
-{
-    bool blocked;
-    if (cn < 0) {                                     // the list overflowed: the walk itself
-        blocked = shadow_blocked(S, cull, o, d, dist, c);
-    } else {
-        const int2 res = scan_first<true>(L, S, o, d, make_raybox(o, d), stride, q, cn >> 2, c);
-        if (res.y < 0) {
-            blocked = (cn & 3) != 0;                  // the walk threw or reached the step cap
-        } else {
-            const RtPrim &pr = S.prim[res.y];
-            Hit h;
-            if (prim_hit(pr, o, d, h) < 0) blocked = true;                  // the winner throws
-            else if (S.shades[pr.meta >> 2].light) blocked = false;
-            else {
-                const double a = h.p[0] - o[0], b = h.p[1] - o[1], f = h.p[2] - o[2];
-                blocked = sqrt(dot3(a, b, f, a, b, f)) < dist - 1e-3;
-            }
-        }
-    }
-    if (!blocked) {
-        double s3[3] = {e.s[0], e.s[1], e.s[2]};
-        shadow_add(L, lt, e.path, dist, cosine, s3);
-        e.s[0] = s3[0]; e.s[1] = s3[1]; e.s[2] = s3[2];
-    }
-}
-
-template <int MINW>
-__global__ void __launch_bounds__(256, MINW) k_shadow_walk(RtLaunch L)
-{
-    TL_SCOPE(L.tl);
-    const int lane = threadIdx.x & 63;
-    const int n = L.ctr[2];
-    const RtFrameSetup F = *L.setup;
-    const RtDevScene &S = L.scene;
-    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
-    const rt_light lt = L.lights[L.shadow_light];
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (;;) {
-        const int base = claim(L.ctr + RT_CTR_SHADOW + 2 * L.shadow_light, lane) * 64;
-        if (base >= n) break;
-        const int q = base + lane;
-        if (q >= n) continue;
-        const RtShadowRec &e = L.shadow_q[q];
-        RaySrc src;
-        double dist, cosine;
-        if (!shadow_ray(lt, e.p, e.n, src.o, src.d, dist, cosine)) {
-            L.cand_n[q] = SHADOW_NO_RAY;
-            continue;
-        }
-        src.valid = true;
-        src.id = (size_t)q;
-        src.pix = e.pix;
-        src.rec = L.ovf;                          // non-null: seated like a continuation
-        walk_item(L, S, F, src, stride, c);
-    }
-}
-
-template <int MINW>
-__global__ void __launch_bounds__(256, MINW) k_shadow_first(RtLaunch L)
-{
-    TL_SCOPE(L.tl);
-    const int lane = threadIdx.x & 63;
-    const int n = L.ctr[2];
-    const RtDevScene &S = L.scene;
-    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
-    const bool cull = L.cull != 0;
-    const rt_light lt = L.lights[L.shadow_light];
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (;;) {
-        const int base = claim(L.ctr + RT_CTR_SHADOW + 2 * L.shadow_light + 1, lane) * 64;
-        if (base >= n) break;
-        const int q = base + lane;
-        if (q >= n) continue;
-        const int cn = L.cand_n[q];
-        if (cn == SHADOW_NO_RAY) continue;
-        RtShadowRec &e = L.shadow_q[q];
-        double o[3], d[3], dist, cosine;
-        shadow_ray(lt, e.p, e.n, o, d, dist, cosine);
-        shadow_decide(L, S, cull, lt, e, o, d, dist, cosine, cn, (uint32_t)stride, (uint32_t)q, c);
-    }
-}
-
-// The deferred matte ends' pixels: colour times the light factor.  Runs after the lights' passes.
+// deferred (L.shadow_q, count ctr[2]), one lane per record: each light's shadow ray searched in the
+// shadow tree (shadow_blocked), the unblocked lights' terms added in light order, the pixel written.
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_shadow(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
     const int n = L.ctr[2];
+    const bool cull = L.cull != 0;
     for (;;) {
         const int base = claim(L.ctr + 3, lane) * 64;
         if (base >= n) break;
         const int q = base + lane;
         if (q >= n) continue;
         const RtShadowRec e = L.shadow_q[q];
+        double s[3];
+        shadow_factor(L.scene, L, cull, e.p, e.n, e.path, s);
         RayResult R;
-        R.rgb[0] = e.col[0] * e.s[0]; R.rgb[1] = e.col[1] * e.s[1]; R.rgb[2] = e.col[2] * e.s[2];
+        R.rgb[0] = e.col[0] * s[0]; R.rgb[1] = e.col[1] * s[1]; R.rgb[2] = e.col[2] * s[2];
         R.hit_ent = e.hit_ent;
         R.hit_node = e.hit_node;
         R.segments = e.segments;
         R.status = ST_OK;
         write_pixel(L, (size_t)e.pix, R);
     }
+}
+
+// ---- the shadow tree (RtShNode) of a scene, built on the device (rt_launch_shadow_tree) ----------------
+// depth[n]: levels below the root (-1: a slot not under the root); *maxd: the deepest
+__global__ void k_sh_depth(RtDevScene S, int32_t *depth, int32_t *maxd)
+{
+    const int n = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (n >= S.n_nodes) return;
+    int d = 0, x = n;
+    while (d <= 4096) {
+        const int p = S.node_up[2 * x];
+        if (p < 0) break;
+        x = p;
+        d++;
+    }
+    d = x == 0 && d <= 4096 ? d : -1;
+    depth[n] = d;
+    if (d > 0) atomicMax(maxd, d);
+}
+
+// Level d, bottom-up: a node's record count (itself and its non-empty subtrees; 0 without entities
+// at or below it) and the union of its own cull-root box and its non-empty children's
+__global__ void k_sh_up(RtDevScene S, const int32_t *depth, int d, int32_t *size, RtShNode *box)
+{
+    const int n = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (n >= S.n_nodes || depth[n] != d) return;
+    const RtNode &nd = S.node[n];
+    RtShNode b;
+    int sz = 0;
+    for (int a = 0; a < 3; a++) { b.lo[a] = INFINITY; b.hi[a] = -INFINITY; }
+    if (nd.n_ent > 0) {
+        for (int a = 0; a < 3; a++) { b.lo[a] = nd.box.lo[a]; b.hi[a] = nd.box.hi[a]; }
+        sz = 1;
+    }
+    for (int c = 0; c < 8; c++) {
+        const int ch = nd.child[c];
+        if (ch < 0 || size[ch] == 0) continue;
+        sz += size[ch];
+        const RtShNode cb = box[ch];
+        for (int a = 0; a < 3; a++) { b.lo[a] = fminf(b.lo[a], cb.lo[a]); b.hi[a] = fmaxf(b.hi[a], cb.hi[a]); }
+    }
+    if (sz > 0 && nd.n_ent == 0) sz++;                 // the node's own record
+    size[n] = sz;
+    b.skip = -1;
+    b.root = nd.n_ent > 0 ? nd.bvh_root : -1;
+    box[n] = b;
+}
+
+// Each non-empty node's record at its pre-order position: climbing to the root, every level adds the
+// parent's record and the records of the earlier (lower octant) non-empty siblings
+__global__ void k_sh_place(RtDevScene S, const int32_t *depth, const int32_t *size, const RtShNode *box, RtShNode *out)
+{
+    const int n = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (n >= S.n_nodes || depth[n] < 0 || size[n] == 0) return;
+    int idx = 0;
+    for (int x = n; x != 0;) {
+        const int p = S.node_up[2 * x];
+        const RtNode &pn = S.node[p];
+        idx++;
+        for (int c = 0; c < 8; c++) {
+            const int ch = pn.child[c];
+            if (ch == x) break;
+            if (ch >= 0) idx += size[ch];
+        }
+        x = p;
+    }
+    RtShNode r = box[n];
+    r.skip = idx + size[n] < size[0] ? idx + size[n] : -1;
+    out[idx] = r;
 }
 
 // A narrow bounce level as ONE launch (L.level_solo): where a recent frame predicts a
@@ -2713,15 +2729,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
         launch_persistent(k_cont<3>, st, Lc,
                           cont_hint == 0 && RT_NO_OP_BLOCKS > 0 && L.lv_blocks <= 0 ? RT_NO_OP_BLOCKS : level_blocks(L, cont_hint));
         // shadow rays (rt_set_lights): the deferred matte ends, after every pass that defers them
-        if (L.shadow_q) {
-            for (int l = 0; l < L.n_lights; l++) {
-                RtLaunch Ls = Lc;
-                Ls.shadow_light = l;
-                launch_persistent(k_shadow_walk<4>, st, Ls);
-                launch_persistent(k_shadow_first<4>, st, Ls);
-            }
-            launch_persistent(k_shadow<8>, st, Lc);
-        }
+        if (L.shadow_q) launch_persistent(k_shadow<4>, st, Lc);
         // this frame's counters come back for the next frames' grid hints (any recent frame will do)
         if (L.ctr_out) {
             HIP_TRY(hipMemcpyAsync(L.ctr_out, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
@@ -2730,6 +2738,33 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
     }
     HIP_TRY(hipGetLastError());
     if (ev_end) HIP_TRY(hipEventRecord((hipEvent_t)ev_end, st));
+    return RT_OK;
+}
+
+int rt_launch_shadow_tree(const RtDevScene &S, RtShNode *tmp, RtShNode *out, int32_t *ints, void *stream,
+                          int32_t *n_out)
+{
+    hipStream_t st = (hipStream_t)stream;
+    const int N = S.n_nodes;
+    *n_out = 0;
+    if (N <= 0) return RT_OK;
+    int32_t *depth = ints, *size = ints + N, *maxd = ints + 2 * (size_t)N;
+    const dim3 grid((N + 255) / 256), block(256);
+    HIP_TRY(hipMemsetAsync(maxd, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(k_sh_depth, grid, block, 0, st, S, depth, maxd);
+    HIP_TRY(hipGetLastError());
+    int32_t D = 0;
+    HIP_TRY(hipMemcpyAsync(&D, maxd, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int d = D; d >= 0; d--) hipLaunchKernelGGL(k_sh_up, grid, block, 0, st, S, (const int32_t *)depth, d, size, tmp);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_sh_place, grid, block, 0, st, S, (const int32_t *)depth, (const int32_t *)size,
+                       (const RtShNode *)tmp, out);
+    HIP_TRY(hipGetLastError());
+    int32_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, size, sizeof(int32_t), hipMemcpyDeviceToHost, st));   // size[0]: the root's
+    HIP_TRY(hipStreamSynchronize(st));
+    *n_out = total;
     return RT_OK;
 }
 
@@ -2776,8 +2811,7 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *na
             {(const void *)k_first<4>, "k_first"}, {(const void *)k_first<6>, "k_first"}, {(const void *)k_first<8>, "k_first"},
 
             {(const void *)k_shade<3>, "k_shade"}, {(const void *)k_shade<4>, "k_shade"}, {(const void *)k_shade<5>, "k_shade"},
-            {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<8>, "k_shadow"},
-            {(const void *)k_shadow_walk<4>, "k_shadow_walk"}, {(const void *)k_shadow_first<4>, "k_shadow_first"}};
+            {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<4>, "k_shadow"}};
         for (int i = 0; i < n; i++) {
             for (int q = 0; q < 4; q++) rec4[4 * i + q] = v[4 * i + q];
             const char *nm = "?";

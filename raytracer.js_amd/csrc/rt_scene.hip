@@ -505,6 +505,8 @@ struct RtSceneStore {
         d.n_bvh = (int32_t)bvh_used;
         d.n_top = n_top;
         d.bvh_leaf = leaf;
+        d.shnode = nullptr;                            // the context builds it for frames with lights
+        d.n_sh = 0;
 #ifdef RT_NO_EXACT_SLOTS
         d.exact_slots = 0;                             // A/B builds: the general plane computation only
 #else

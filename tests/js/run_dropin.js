@@ -116,6 +116,14 @@ if (ri > 0) {
 	fs.writeFileSync(out_prefix + '.repeat.json', JSON.stringify({ frame_ms: ms_plain, frame_ms_stats: ms_counted }));
 }
 
+// --reopen: close() the context, then trace again: the next frame makes a new context, which must get
+// the light list too (the drop-in keeps it; ADVICE r4)
+if (process.argv.includes('--reopen')) {
+	tracer.close();
+	tracer.trace_frame();
+	fs.writeFileSync(out_prefix + '.3.rgb', Buffer.from(eb.pixels.buffer));
+}
+
 const ei = process.argv.indexOf('--edit');
 if (ei > 0) {
 	const [A, B, C, px, py, pz, depth] = process.argv.slice(ei + 1, ei + 8).map(Number);

@@ -36,9 +36,9 @@ def test_more_gpus_than_the_host_has_fails():
 def test_kernel_names_and_rooflines():
     import bench
     assert bench._kernel_base("(anonymous namespace)::k_walk<4>(RtLaunch)") == "k_walk"
-    assert bench._kernel_base("void (anonymous namespace)::k_walk_seg<2>(RtLaunch)") == "k_walk_seg"
-    assert bench._kernel_base("k_first_seg<4>") == "k_first_seg"
-    dur = {"k_walk": 2.0, "k_walk_seg": 0.5, "k_first": 1.0}
+    assert bench._kernel_base("void (anonymous namespace)::k_walk_refill<4>(RtLaunch)") == "k_walk_refill"
+    assert bench._kernel_base("k_shadow<4>") == "k_shadow"
+    dur = {"k_walk": 2.0, "k_walk_refill": 0.5, "k_first": 1.0}
     pmc = {"k_walk": dict(FETCH_SIZE=1000.0, WRITE_SIZE=500.0, SQ_INSTS_VALU=1e9, SQ_INSTS_VALU_ADD_F64=1e8,
                           SQ_INSTS_VALU_MUL_F64=1e8, SQ_INSTS_VALU_FMA_F64=0.0, SQ_INSTS_VALU_TRANS_F64=0.0,
                           GRBM_GUI_ACTIVE=8 * 2.0e9 * 2e-3, SQ_ACTIVE_INST_VALU=1e9, SQ_THREAD_CYCLES_VALU=4e10,
@@ -53,10 +53,10 @@ def test_kernel_names_and_rooflines():
     assert w["valu_issue_frac"] == pytest.approx(cyc / (1024 * 2.0e9 * 2e-3), rel=1e-3)
     assert w["active_lanes"] == pytest.approx(40.0) and w["wait_frac"] == pytest.approx(0.3)
     assert w["binding_roof"] == "valu-issue"
-    # the walk pass's algorithmic bytes are split between k_walk and k_walk_seg by time
+    # the walk pass's algorithmic bytes are split between k_walk and k_walk_refill by time
     walk_bytes = 48 * 10 + 32 * 20 + 40 * 30
-    assert w["alg_bytes_cache_served_pooled"] + kr["k_walk_seg"]["alg_bytes_cache_served_pooled"] == pytest.approx(walk_bytes, abs=2)
-    assert list(kr) == ["k_walk", "k_first", "k_walk_seg"]          # by time
+    assert w["alg_bytes_cache_served_pooled"] + kr["k_walk_refill"]["alg_bytes_cache_served_pooled"] == pytest.approx(walk_bytes, abs=2)
+    assert list(kr) == ["k_walk", "k_first", "k_walk_refill"]          # by time
 
 
 def test_usable_cores_reports_quota():
@@ -70,7 +70,7 @@ def test_fused_level0_pools_walk_and_first_bytes():
     """With k_walk_first in the trace the walk and first-hit passes' algorithmic bytes
     are one pool, shared by every walk / first-hit kernel in proportion to its time."""
     import bench
-    dur = {"k_walk_first": 3.0, "k_walk_seg": 0.5, "k_first_seg": 0.5}
+    dur = {"k_walk_first": 3.0, "k_level": 0.5, "k_walk_refill": 0.25, "k_first": 0.25}
     counters = dict(n_ret=10, n_slot=20, n_loc=30, n_cull=40, n_exact=50, n_hit=60, segments=70, primary=7)
     kr = bench.kernel_rooflines(dur, {}, counters)
     pool = 48 * 10 + 32 * 20 + 40 * 30 + 32 * 40 + 80 * 50

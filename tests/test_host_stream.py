@@ -130,3 +130,38 @@ def test_streamed_keeps_the_reference_partial_frame(blend, ids, monkeypatch):
     assert not np.array_equal(got["rgb"].view(np.uint32), old.view(np.uint32))
     if ids:
         assert np.array_equal(got["status"], want["status"])
+
+
+@pytest.mark.parametrize("cap", [None, FORCE])
+def test_lit_host_frames_equal_the_oracle(small3, cap, monkeypatch):
+    """Shadow lights: every matte pixel is written by k_shadow after level 0, so a lit frame
+    is never streamed (the late list would hold most of the frame); with streaming on and forced, three
+    lit host frames on one context (hints from the second on) equal the one-launch frame and the oracle,
+    ids and a blend included, and a frame after the lights are turned off streams again."""
+    spec, scene = small3
+    lights = [((0.25, 0.75, 0.25), (0.6, 0.5, 0.4)), ((0.5, 0.9, 0.6), (0.2, 0.2, 0.2))]
+    cam = scenes.make_camera(160, 120)
+    for blend in (1.0, 0.5):
+        cfg = scenes.make_config(4, col_weight=blend)
+        old = np.random.default_rng(2).random(160 * 120 * 3).astype(np.float32)
+        w, root = oracle.build_scene(spec)
+        w.set_lights(lights, 0.1)
+        ref = w.trace_frame(root, cam, cfg, rgb=old.copy(), nthreads=8)
+        a, b = _ctx(scene, monkeypatch, True, cap), _ctx(scene, monkeypatch, False)
+        try:
+            a.set_lights(lights, 0.1)
+            b.set_lights(lights, 0.1)
+            one = b.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True)
+            for _ in range(3):
+                got = a.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True)
+                _same(got, one)
+                for k in KEYS:
+                    assert np.array_equal(ref[k].view(np.uint8), got[k].view(np.uint8)), k
+            a.set_lights([])
+            w.set_lights([])
+            plain = a.trace_frame(cam, cfg, rgb=old.copy(), allow_fault=True)
+            ref0 = w.trace_frame(root, cam, cfg, rgb=old.copy(), nthreads=8)
+            assert np.array_equal(ref0["rgb"].view(np.uint32), plain["rgb"].view(np.uint32))
+        finally:
+            a.close()
+            b.close()

@@ -191,8 +191,10 @@ def test_dropin_shadow_rays_equal_oracle(tmp_path, plain):
     lights = [((0.25, 0.75, 0.25), (0.6, 0.5, 0.4)), ((0.5, 0.9, 0.6), (0.2, 0.2, 0.2))]
     path = _dump(tmp_path, spec, cam, cfg)
     arg = json.dumps({"lights": [{"pos": list(p), "rgb": list(c)} for p, c in lights], "ambient": 0.15})
-    _node([RUNNER, path, str(tmp_path / "out"), "--lights", arg] + (["--plain"] if plain else []))
+    _node([RUNNER, path, str(tmp_path / "out"), "--lights", arg, "--reopen"] + (["--plain"] if plain else []))
     rgb = np.fromfile(tmp_path / "out.rgb", dtype=np.float32)
+    # after close(), the next trace_frame()'s new context renders with the same lights
+    assert np.array_equal(np.fromfile(tmp_path / "out.3.rgb", dtype=np.float32).view(np.uint32), rgb.view(np.uint32))
     w, root = oracle.build_scene(spec)
     w.set_lights(lights, 0.15)
     ref = w.trace_frame(root, cam, cfg, nthreads=8)
