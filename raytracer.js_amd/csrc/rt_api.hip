@@ -82,7 +82,7 @@ struct RtDevice {
     hipStream_t stream = nullptr;
     RtDevScene scene{};
     DevBuf b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters,
-        b_fault, b_lights, b_shadow, b_sh, b_sh_tmp, b_sh_ints;
+        b_fault, b_lights, b_shadow, b_sh, b_sh_tmp, b_sh_ints, b_gr[4];
     uint64_t lights_seq = 0;                     // the rt_set_lights call b_lights holds
     uint64_t sh_epoch = 0;                       // the scene (store epoch) b_sh's shadow tree was built for
     std::vector<std::array<hipEvent_t, 2>> ev;   // trace-kernel timing ring
@@ -106,6 +106,8 @@ struct rt_ctx {
     bool split = true;               // walk pass + test pass (RT_SPLIT=0: fused k_trace)
     int n_lights = 0;                // rt_set_lights: shadow rays (a build extension; 0 = off)
     int stream_gated = 0;            // host frames the streaming gate declined since dev[0]'s last count
+    int shadow_grid = 0;             // shadow rays' grid cells per axis (RT_SHADOW_GRID; 0: from the primitive count,
+                                     // -1: no grid, the tree search)
     double ambient = 0;
     rt_light lights[RT_MAX_LIGHTS] = {};
     uint64_t lights_seq = 0;         // bumped per rt_set_lights; a device uploads at its next frame
@@ -275,6 +277,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_LATE_CAP")) c->late_cap = atoll(e) < 0 ? 0 : atoll(e);
     if (const char *e = getenv("RT_STREAM_SPLIT")) c->stream_split = atoi(e) != 0;
     if (const char *e = getenv("RT_HOST_DIRECT")) c->host_direct = atoi(e) != 0;
+    if (const char *e = getenv("RT_SHADOW_GRID")) c->shadow_grid = atoi(e);
     if (const char *e = getenv("RT_BANDS")) c->bands = atoi(e) < 1 ? 1 : (atoi(e) > RT_MAX_BANDS ? RT_MAX_BANDS : atoi(e));
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
     // parts on one GPU) gathers by device copies, as RT_CREATE_PEER_GATHER asks for.  RT_GATHER
@@ -597,7 +600,7 @@ static int ensure_shadow_tree(rt_ctx *c, RtDevice &d)
             if (b.stream) HIP_TRY(hipStreamSynchronize(b.stream));
     const size_t N = (size_t)std::max(d.scene.n_nodes, 1);
     if ((r = d.b_sh.ensure(sizeof(RtShNode) * N)) != RT_OK || (r = d.b_sh_tmp.ensure(sizeof(RtShNode) * N)) != RT_OK ||
-        (r = d.b_sh_ints.ensure(sizeof(int32_t) * (2 * N + 2))) != RT_OK)
+        (r = d.b_sh_ints.ensure(sizeof(int32_t) * (2 * N + 4))) != RT_OK)
         return r;
     int32_t n_sh = 0;
     if ((r = rt_launch_shadow_tree(d.scene, (RtShNode *)d.b_sh_tmp.p, (RtShNode *)d.b_sh.p, (int32_t *)d.b_sh_ints.p,
@@ -605,6 +608,15 @@ static int ensure_shadow_tree(rt_ctx *c, RtDevice &d)
         return r;
     d.scene.shnode = (const RtShNode *)d.b_sh.p;
     d.scene.n_sh = n_sh;
+    // the uniform grid the shadow rays search (RT_SHADOW_GRID: cells per axis; 0: from the primitive
+    // count; -1: none, the tree search)
+    auto alloc = [](void *ctx, size_t bytes, int which) -> void * {
+        DevBuf &b = static_cast<RtDevice *>(ctx)->b_gr[which];
+        return b.ensure(bytes) == RT_OK ? b.p : nullptr;
+    };
+    if (c->shadow_grid >= 0 &&
+        (r = rt_launch_shadow_grid(&d.scene, (const int32_t *)d.b_sh_ints.p, c->shadow_grid, alloc, &d, d.stream)) != RT_OK)
+        return r;
     d.sh_epoch = ep;
     return RT_OK;
 }
@@ -719,6 +731,13 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
         if ((r = use_device(d)) != RT_OK) return r;
         d.scene.shnode = ph.scene.shnode;
         d.scene.n_sh = ph.scene.n_sh;
+        d.scene.g_cell = ph.scene.g_cell;
+        d.scene.g_ref = ph.scene.g_ref;
+        d.scene.g_big = ph.scene.g_big;
+        d.scene.g_res = ph.scene.g_res;
+        d.scene.g_nbig = ph.scene.g_nbig;
+        d.scene.g_cs = ph.scene.g_cs;
+        for (int a = 0; a < 3; a++) d.scene.g_lo[a] = ph.scene.g_lo[a];
         L.scene = d.scene;
     }
     if (c->split && P > 0 && ((int64_t)P > c->fuse_max || (int64_t)d.scene.n_list > c->fuse_list)) {

@@ -108,6 +108,15 @@ struct RtDevScene {
                                 // entities is one leaf: its prims at node_ent.x in order)
     const RtShNode *shnode;     // shadow rays' search tree, n_sh records (null until a frame with lights
     int32_t n_sh;               // builds it: rt_api.hip ensure_shadow_tree)
+    // shadow rays' uniform grid (rt_launch_shadow_tree): g_res^3 cells of size g_cs from
+    // g_lo; cell c's entries are g_ref[g_cell[c] .. g_cell[c + 1]) (the primitive's box and slot:
+    // RtBvh.info = prim slot), g_big lists the primitives too large for cells (or reaching outside
+    // the grid); g_res = 0: no grid (the tree search runs)
+    const uint32_t *g_cell;
+    const RtBvh *g_ref;
+    const RtBvh *g_big;
+    int32_t g_res, g_nbig;
+    float g_lo[3], g_cs;
 };
 
 // A ray of the split path at its first continuation (segment start after a mirror / transmission
@@ -198,6 +207,9 @@ void rt_builder_synced(rt_builder *b, const RtSceneStore *st, uint64_t epoch, bo
 int rt_store_apply_edit(RtSceneStore *st, const RtEdit &e, const rt_shade *shades, int32_t n_shades,
                         const double *substance_ri, int32_t n_substances, RtDevScene *dev, rt_update_stats *stats);
 
+// The cull boxes' widening delta and the SAH clamp of a scene, from its root cube (rt_cull.cpp).
+void rt_cull_scale(const double root_pos[3], double root_size, double *delta, double *clampv);
+
 // Kernel launchers (rt_kernels.hip).
 struct RtLaunch {
     RtDevScene scene;
@@ -283,10 +295,18 @@ int rt_launch_exposure_stats(const float *d_rgb, long long n, double *d_partials
 int rt_launch_tonemap(const float *d_rgb, long long n, double low, double high, uint8_t *d_rgba, void *stream);
 int rt_launch_debug_walk(const RtDevScene &S, const double o[3], const double d[3], int include_undefined,
                          int max_out, int32_t *d_tree, int32_t *d_oct, int32_t *d_n, void *stream);
-// The shadow tree of scene S into out[0 .. *n_out) (tmp: S.n_nodes records, ints: 2 * S.n_nodes + 2
-// int32 of scratch).  Synchronises `stream` twice (the deepest level, the record count).
+// The shadow tree of scene S into out[0 .. *n_out) (tmp: S.n_nodes records, ints: 2 * S.n_nodes + 4
+// int32 of scratch).  Synchronises `stream` twice.
 int rt_launch_shadow_tree(const RtDevScene &S, RtShNode *tmp, RtShNode *out, int32_t *ints, void *stream,
                           int32_t *n_out);
+// Shadow rays' uniform grid over scene S's primitives (res^3 cells over the root cube; 0 picks res
+// from the primitive count), over the node slots whose depth[] (rt_launch_shadow_tree's scratch) is
+// >= 0.  `alloc(bytes, which)` returns device memory for buffer `which` (0 cell counts / offsets, 1 cell
+// entries, 2 large primitives, 3 scan scratch), kept by the caller; the grid's fields are written into
+// *S (g_res stays 0 when the scene admits no grid).  Synchronises `stream`.
+typedef void *(*RtGridAlloc)(void *ctx, size_t bytes, int which);
+int rt_launch_shadow_grid(RtDevScene *S, const int32_t *depth, int res, RtGridAlloc alloc, void *alloc_ctx,
+                          void *stream);
 
 // ---- multi-device frame assembly (rt_multi.hip) -------------------------------------------------------
 // Rows between a frame (H rows of row_bytes) and the stacked parts (n_parts x max_rows rows):

@@ -1286,19 +1286,13 @@ __device__ __forceinline__ bool prim_blocks(const RtDevScene &S, int slot, const
     return sqrt(dot3(a, b, e, a, b, e)) < lim;
 }
 
-// The shadow ray from q along u (unit) toward a light at distance dist (from the hit point, q being
-// 1e-3 along u from it).  Culling off (or a ray the f32 boxes cannot serve: rb.ok) tests every entity.
-// Why the pruning is exact: a blocking hit lies within its entity's widened box at a parameter below
+// The tree search (RtShNode records, pre-order with skips): every non-empty subtree's union box is
+// tested, then a visited node's own cull hierarchy.  Why the pruning is exact: a blocking hit lies within its entity's widened box at a parameter below
 // dist - 1e-3 (|u| = 1 to an ulp), and the f32 slab test errs far less than the widening (§5.1), so
 // its box, and every enclosing union, passes the segment test up to tlim >= dist.
-__device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, const double q[3], const double u[3],
-                                            double dist)
+__device__ __forceinline__ bool shadow_blocked_tree(const RtDevScene &S, const RayBox &rb, bool prune, float tlim,
+                                                 const double q[3], const double u[3], double lim)
 {
-    const RayBox rb = make_raybox(q, u);
-    const bool prune = cull && rb.ok;
-    float tlim = (float)(dist * 1.0001);
-    if (!(tlim >= 0.0f)) tlim = INFINITY;
-    const double lim = dist - 1e-3;
     int k = S.n_sh > 0 ? 0 : -1, i = -1, slot = 0, end = 0;
     for (;;) {
         if (slot < end) {
@@ -1321,6 +1315,78 @@ __device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, c
             return false;
         }
     }
+}
+
+// The grid search: the large primitives' list (S.g_big), then the cells the segment
+// [0, tlim] crosses, in order (a 3D DDA in f32: the next cell is the one whose boundary the segment
+// meets first, each boundary parameter computed from the integer cell index, no accumulation), each
+// cell's entries tested by their box and then exactly.  A primitive is entered in every cell its box
+// (widened by delta, §5.1) overlaps: where f32 rounding steps the DDA into a neighbour near a cell
+// boundary, the blocking point lies within delta of that neighbour too, so its primitive is listed
+// there (delta exceeds the DDA's f32 error by orders of magnitude).
+__device__ __forceinline__ bool shadow_blocked_grid(const RtDevScene &S, const RayBox &rb, float tlim,
+                                                 const double q[3], const double u[3], double lim)
+{
+    for (int b = 0; b < S.g_nbig; b++) {
+        const RtBvh e = S.g_big[b];
+        if (ray_box_seg(e.lo, e.hi, rb, tlim) && prim_blocks(S, e.info, q, u, lim)) return true;
+    }
+    const int res = S.g_res;
+    const float cs = S.g_cs, ext = cs * (float)res;
+    const float o[3] = {rb.ox, rb.oy, rb.oz}, iv[3] = {rb.ix, rb.iy, rb.iz};
+    const float uf[3] = {(float)u[0], (float)u[1], (float)u[2]};
+    float t0 = 0.0f, t1 = tlim;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float ta = (S.g_lo[a] - o[a]) * iv[a], tb = (S.g_lo[a] + ext - o[a]) * iv[a];
+        t0 = fmaxf(t0, fminf(ta, tb));
+        t1 = fminf(t1, fmaxf(ta, tb));
+    }
+    if (!(t0 <= t1)) return false;
+    int c[3], stp[3];
+    float tm[3];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float f = floorf((o[a] + uf[a] * t0 - S.g_lo[a]) / cs);
+        c[a] = f < 0.0f ? 0 : (f >= (float)res ? res - 1 : (int)f);
+        stp[a] = uf[a] > 0.0f ? 1 : (uf[a] < 0.0f ? -1 : 0);
+        tm[a] = stp[a] == 0 ? INFINITY : ((float)(c[a] + (stp[a] > 0)) * cs + S.g_lo[a] - o[a]) * iv[a];
+    }
+    uint32_t r = 0, re = 0;
+    bool load = true;
+    for (;;) {
+        if (r < re) {
+            const RtBvh e = S.g_ref[r++];
+            if (ray_box_seg(e.lo, e.hi, rb, tlim) && prim_blocks(S, e.info, q, u, lim)) return true;
+        } else if (load) {
+            const uint32_t cell = ((uint32_t)c[2] * (uint32_t)res + (uint32_t)c[1]) * (uint32_t)res + (uint32_t)c[0];
+            r = S.g_cell[cell];
+            re = S.g_cell[cell + 1];
+            load = false;
+        } else {
+            const int a = tm[0] <= tm[1] ? (tm[0] <= tm[2] ? 0 : 2) : (tm[1] <= tm[2] ? 1 : 2);
+            if (!(tm[a] <= t1)) return false;                    // the segment ends in this cell
+            c[a] += stp[a];
+            if ((unsigned)c[a] >= (unsigned)res) return false;   // it leaves the grid
+            tm[a] = ((float)(c[a] + (stp[a] > 0)) * cs + S.g_lo[a] - o[a]) * iv[a];
+            load = true;
+        }
+    }
+}
+
+// The shadow ray from q along u (unit) toward a light at distance dist (from the hit point, q being
+// 1e-3 along u from it): the grid search, or the tree search where no grid was built; culling off (or
+// a ray the f32 boxes cannot serve: rb.ok) tests every entity.
+__device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, const double q[3], const double u[3],
+                                            double dist)
+{
+    const RayBox rb = make_raybox(q, u);
+    const bool prune = cull && rb.ok;
+    float tlim = (float)(dist * 1.0001);
+    if (!(tlim >= 0.0f)) tlim = INFINITY;
+    const double lim = dist - 1e-3;
+    if (prune && S.g_res > 0) return shadow_blocked_grid(S, rb, tlim, q, u, lim);
+    return shadow_blocked_tree(S, rb, prune, tlim, q, u, lim);
 }
 
 // The shadow ray of a matte hit (point p, normal nrm) toward light lt: false when the light is
@@ -2473,6 +2539,172 @@ __global__ void k_sh_place(RtDevScene S, const int32_t *depth, const int32_t *si
     out[idx] = r;
 }
 
+// ---- the shadow grid (rt_launch_shadow_grid) -----------------------------------------------------------
+__device__ __forceinline__ float f32_down(double x)
+{
+    float f = (float)x;
+    if (isnan(x)) return -INFINITY;
+    if ((double)f > x) f = nextafterf(f, -INFINITY);
+    return f;
+}
+__device__ __forceinline__ float f32_up(double x)
+{
+    float f = (float)x;
+    if (isnan(x)) return INFINITY;
+    if ((double)f < x) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+// A primitive's conservative box, the cull boxes' rule (rt_cull.cpp prim_bounds): its geometry's
+// bounds widened by delta, rounded outward to f32; false (unbounded) for non-finite geometry and for
+// skinny triangles, whose Moller-Trumbore test may report hits off the widened box.
+__device__ bool prim_box(const RtPrim &p, double delta, float lo[3], float hi[3])
+{
+    const int type = p.meta & 3;
+    const double *g = p.g;
+    double l[3], h[3];
+    bool finite = true;
+    if (type == RT_ENT_SPHERE) {
+        const double r = 1.0 / fabs(g[6]);
+        for (int a = 0; a < 3; a++) { l[a] = g[a] - r; h[a] = g[a] + r; }
+        finite = isfinite(r);
+    } else if (type == RT_ENT_BOX) {
+        const double hs = fabs(g[3]) * 0.5;
+        for (int a = 0; a < 3; a++) { l[a] = g[a] - hs; h[a] = g[a] + hs; }
+    } else {
+        double l1 = 0, l2 = 0, l3 = 0;
+        for (int a = 0; a < 3; a++) {
+            const double v0 = g[a], v1 = g[a] + g[3 + a], v2 = g[a] + g[6 + a];
+            l[a] = fmin(v0, fmin(v1, v2));
+            h[a] = fmax(v0, fmax(v1, v2));
+            l1 += g[3 + a] * g[3 + a];
+            l2 += g[6 + a] * g[6 + a];
+            l3 += (g[6 + a] - g[3 + a]) * (g[6 + a] - g[3 + a]);
+        }
+        const double L2 = fmax(l1, fmax(l2, l3));
+        const double cx = g[4] * g[8] - g[5] * g[7], cy = g[5] * g[6] - g[3] * g[8], cz = g[3] * g[7] - g[4] * g[6];
+        if (!(cx * cx + cy * cy + cz * cz > 1e-6 * L2 * L2)) finite = false;
+    }
+    for (int a = 0; a < 3; a++) finite = finite && isfinite(l[a]) && isfinite(h[a]) && isfinite(g[a]);
+    for (int a = 0; a < 3; a++) {
+        lo[a] = finite ? f32_down(l[a] - delta) : -INFINITY;
+        hi[a] = finite ? f32_up(h[a] + delta) : INFINITY;
+    }
+    return finite;
+}
+
+struct GridDims {
+    float lo[3], cs, inv;
+    int res;
+};
+constexpr int GRID_BIG_CELLS = 64;          // a primitive over more cells goes to the large list
+
+// The cells a primitive's box overlaps (one cell's worth of slack at each end is not needed: the box
+// is already widened), or false when it goes to the large list: unbounded, reaching outside the grid,
+// or over more than GRID_BIG_CELLS cells.
+__device__ __forceinline__ bool grid_range(const GridDims &G, const float lo[3], const float hi[3], bool bounded,
+                                           int i0[3], int i1[3])
+{
+    if (!bounded) return false;
+    long long cells = 1;
+    for (int a = 0; a < 3; a++) {
+        const float fa = (lo[a] - G.lo[a]) * G.inv, fb = (hi[a] - G.lo[a]) * G.inv;
+        if (!(fa >= 0.0f && fb < (float)G.res)) return false;
+        i0[a] = (int)fa;
+        i1[a] = (int)fb;
+        if (i1[a] < i0[a]) i1[a] = i0[a];
+        cells *= i1[a] - i0[a] + 1;
+    }
+    return cells <= GRID_BIG_CELLS;
+}
+
+// Pass 1 (count) / pass 2 (fill): one block per node slot (grid-stride), its threads over the node's
+// primitives.  Count: entries per cell, and the large list's length.  Fill: each cell's entries at
+// start[cell] + (its next free place), the large list in any order.
+template <bool FILL>
+__global__ void __launch_bounds__(256) k_gr_pass(RtDevScene S, GridDims G, double delta, const int32_t *depth,
+                                                uint32_t *count, const uint32_t *start, RtBvh *ref, RtBvh *big,
+                                                int32_t *nbig)
+{
+    for (int n = blockIdx.x; n < S.n_nodes; n += gridDim.x) {
+        if (depth[n] < 0) continue;                              // a slot not under the root
+        const int4 ne = reinterpret_cast<const int4 *>(S.node_ent)[n];   // {prim begin, count, ...}
+        for (int j = threadIdx.x; j < ne.y; j += blockDim.x) {
+            const int slot = ne.x + j;
+            RtBvh e;
+            const bool bounded = prim_box(S.prim[slot], delta, e.lo, e.hi);
+            e.skip = 0;
+            e.info = slot;
+            int i0[3], i1[3];
+            if (!grid_range(G, e.lo, e.hi, bounded, i0, i1)) {
+                const int k = atomicAdd(nbig, 1);
+                if (FILL) big[k] = e;
+                continue;
+            }
+            for (int z = i0[2]; z <= i1[2]; z++)
+                for (int y = i0[1]; y <= i1[1]; y++)
+                    for (int x = i0[0]; x <= i1[0]; x++) {
+                        const uint32_t cell = ((uint32_t)z * (uint32_t)G.res + (uint32_t)y) * (uint32_t)G.res + (uint32_t)x;
+                        const uint32_t k = atomicAdd(&count[cell], 1u);
+                        if (FILL) ref[start[cell] + k] = e;
+                    }
+        }
+    }
+}
+
+// Exclusive scan of n uint32 (in place into out): per block of 2048 its local offsets and total, the
+// totals scanned by one block, then added back.
+constexpr int SCAN_PER = 8, SCAN_BLOCK = 2048;
+__global__ void __launch_bounds__(256) k_scan_local(const uint32_t *in, uint32_t *out, uint32_t *tot, int n)
+{
+    __shared__ uint32_t sh[256];
+    const int base = blockIdx.x * SCAN_BLOCK + threadIdx.x * SCAN_PER;
+    uint32_t v[SCAN_PER], s = 0;
+    for (int k = 0; k < SCAN_PER; k++) {
+        v[k] = base + k < n ? in[base + k] : 0u;
+        s += v[k];
+    }
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        const uint32_t x = threadIdx.x >= (unsigned)off ? sh[threadIdx.x - off] : 0u;
+        __syncthreads();
+        sh[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint32_t run = sh[threadIdx.x] - s;                            // exclusive within the block
+    for (int k = 0; k < SCAN_PER; k++) {
+        if (base + k < n) out[base + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 255) tot[blockIdx.x] = sh[255];
+}
+__global__ void __launch_bounds__(256) k_scan_tops(uint32_t *tot, int nb)
+{
+    __shared__ uint32_t sh[256];
+    uint32_t carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += 256) {
+        const int i = b0 + (int)threadIdx.x;
+        const uint32_t s = i < nb ? tot[i] : 0u;
+        sh[threadIdx.x] = s;
+        __syncthreads();
+        for (int off = 1; off < 256; off <<= 1) {
+            const uint32_t x = threadIdx.x >= (unsigned)off ? sh[threadIdx.x - off] : 0u;
+            __syncthreads();
+            sh[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if (i < nb) tot[i] = carry + sh[threadIdx.x] - s;
+        carry += sh[255];
+        __syncthreads();
+    }
+}
+__global__ void __launch_bounds__(256) k_scan_add(uint32_t *out, const uint32_t *tot, int n)
+{
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < n) out[i] += tot[i / SCAN_BLOCK];
+}
+
 // A narrow bounce level as ONE launch (L.level_solo): where a recent frame predicts a
 // segmented level that k_seg shades, the host launches this kernel alone instead of the level's five
 // kernels of which four return at once (k_walk, k_seg<false>, k_first, k_shade; in flight each such
@@ -2765,6 +2997,77 @@ int rt_launch_shadow_tree(const RtDevScene &S, RtShNode *tmp, RtShNode *out, int
     HIP_TRY(hipMemcpyAsync(&total, size, sizeof(int32_t), hipMemcpyDeviceToHost, st));   // size[0]: the root's
     HIP_TRY(hipStreamSynchronize(st));
     *n_out = total;
+    return RT_OK;
+}
+
+int rt_launch_shadow_grid(RtDevScene *S, const int32_t *depth, int res, RtGridAlloc alloc, void *actx, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    S->g_res = 0;
+    S->g_nbig = 0;
+    S->g_cell = nullptr;
+    S->g_ref = nullptr;
+    S->g_big = nullptr;
+    const int N = S->n_nodes;
+    if (N <= 0 || S->n_list <= 0) return RT_OK;
+    if (res <= 0) {                                   // about one primitive per cell, 8 .. 256 per axis
+        res = 8;
+        while (res < 256 && (double)res * res * res < (double)S->n_list) res *= 2;
+    }
+    res = std::min(512, std::max(2, res));
+    RtNode root;
+    HIP_TRY(hipMemcpyAsync(&root, S->node, sizeof(RtNode), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const double rp[3] = {root.x, root.y, root.z};
+    double delta = 0, clampv = 0;
+    rt_cull_scale(rp, root.s, &delta, &clampv);
+    if (!(delta > 0 && isfinite(delta) && root.s > 0 && isfinite(root.s))) return RT_OK;
+    // the root cube widened by about 2 delta each side (in f32; a primitive whose box does not fit
+    // inside goes to the large list, so the domain's own rounding only moves primitives there)
+    GridDims G;
+    G.res = res;
+    G.cs = (float)((root.s + 5 * delta) / res) * (1 + 1e-6f);
+    G.inv = 1.0f / G.cs;
+    for (int a = 0; a < 3; a++) G.lo[a] = (float)(rp[a] - 2.5 * delta);
+    const size_t n_cells = (size_t)res * res * res;
+    uint32_t *count = (uint32_t *)alloc(actx, sizeof(uint32_t) * (2 * n_cells + 2), 0);
+    const int nb = (int)((n_cells + 1 + SCAN_BLOCK - 1) / SCAN_BLOCK);
+    uint32_t *tops = (uint32_t *)alloc(actx, sizeof(uint32_t) * (size_t)(nb + 4), 3);
+    if (!count || !tops) return rt_set_error(RT_E_HIP, "shadow grid: out of device memory");
+    uint32_t *start = count + n_cells + 1;                       // n_cells + 1 offsets
+    int32_t *nbig = (int32_t *)(tops + nb + 1);
+    HIP_TRY(hipMemsetAsync(count, 0, sizeof(uint32_t) * (n_cells + 1), st));
+    HIP_TRY(hipMemsetAsync(nbig, 0, sizeof(int32_t), st));
+    const int blocks = (int)std::min<long long>(N, 1 << 16);
+    hipLaunchKernelGGL(k_gr_pass<false>, dim3(blocks), dim3(256), 0, st, *S, G, delta, depth, count,
+                       (const uint32_t *)nullptr, (RtBvh *)nullptr, (RtBvh *)nullptr, nbig);
+    HIP_TRY(hipGetLastError());
+    const int nsc = (int)(n_cells + 1);
+    hipLaunchKernelGGL(k_scan_local, dim3(nb), dim3(256), 0, st, (const uint32_t *)count, start, tops, nsc);
+    hipLaunchKernelGGL(k_scan_tops, dim3(1), dim3(256), 0, st, tops, nb);
+    hipLaunchKernelGGL(k_scan_add, dim3((nsc + 255) / 256), dim3(256), 0, st, start, (const uint32_t *)tops, nsc);
+    HIP_TRY(hipGetLastError());
+    uint32_t n_ref = 0;
+    int32_t n_big = 0;
+    HIP_TRY(hipMemcpyAsync(&n_ref, start + n_cells, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&n_big, nbig, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    RtBvh *ref = (RtBvh *)alloc(actx, sizeof(RtBvh) * ((size_t)n_ref + 1), 1);
+    RtBvh *big = (RtBvh *)alloc(actx, sizeof(RtBvh) * ((size_t)n_big + 1), 2);
+    if (!ref || !big) return rt_set_error(RT_E_HIP, "shadow grid: out of device memory");
+    HIP_TRY(hipMemsetAsync(count, 0, sizeof(uint32_t) * (n_cells + 1), st));
+    HIP_TRY(hipMemsetAsync(nbig, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(k_gr_pass<true>, dim3(blocks), dim3(256), 0, st, *S, G, delta, depth, count,
+                       (const uint32_t *)start, ref, big, nbig);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    S->g_cell = start;
+    S->g_ref = ref;
+    S->g_big = big;
+    S->g_nbig = n_big;
+    S->g_res = res;
+    S->g_cs = G.cs;
+    for (int a = 0; a < 3; a++) S->g_lo[a] = G.lo[a];
     return RT_OK;
 }
 

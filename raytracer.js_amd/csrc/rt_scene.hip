@@ -507,6 +507,11 @@ struct RtSceneStore {
         d.bvh_leaf = leaf;
         d.shnode = nullptr;                            // the context builds it for frames with lights
         d.n_sh = 0;
+        d.g_cell = nullptr;
+        d.g_ref = nullptr;
+        d.g_big = nullptr;
+        d.g_res = 0;
+        d.g_nbig = 0;
 #ifdef RT_NO_EXACT_SLOTS
         d.exact_slots = 0;                             // A/B builds: the general plane computation only
 #else

@@ -622,14 +622,16 @@ class Raytracer {
 
 	_sync_scene() {
 		const a = load_addon();
+		let fresh = false;
 		if (!this._ctx) {
 			const o = this.options;
 			this._ctx = Array.isArray(o.devices) ? a.create(o.devices.map((x) => x | 0), (o.stripe_rows | 0))
 				: a.create(o.device | 0);
+			fresh = true;                   // a new context (first frame, or after close()) holds no scene
 		}
 		const sky = this.config.sky.texture;
 		if (this._scene && loaded_image(sky) && !this._scene._maps.image_index.has(sky)) this._dirty = true;
-		if (!this._scene) {
+		if (!this._scene || fresh) {
 			this._scene = serialize_scene(this.otree, this.config.default_substance, undefined, sky);
 			a.uploadScene(this._ctx, this._scene);
 			const sl = a.sceneSlots(this._ctx, this._scene.node_size.length);

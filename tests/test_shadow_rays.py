@@ -188,6 +188,16 @@ SHADOW_CASES = [
     ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": dict(SPLIT, RT_CAND_CAP="2")}),   # overflow: k_cont defers
     ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": dict(SPLIT, RT_SEG="1")}),        # unsegmented levels
     ("config1", (96, 64), 3, LIGHTS, 0.0, {"blend": 0.25}),
+    # the search over the pre-order tree of union boxes instead of the grid (RT_SHADOW_GRID=-1), split
+    # and fused; grids of 2 cells per axis (most primitives in the large list) and of 256 (each
+    # primitive over many cells, some over more than the cell limit)
+    ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "-1"}}),
+    ("config1", (160, 120), 3, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "-1"}}),
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {}),
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "-1"}}),
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "2"}}),
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "256"}}),
+    ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "3"}}),
 ]
 
 
@@ -196,7 +206,8 @@ SHADOW_CASES = [
 def test_shadow_rays_equal_oracle(monkeypatch, name, wh, refmax, lights, ambient, opt):
     for k, v in opt.get("env", {}).items():
         monkeypatch.setenv(k, v)                      # read at rt_create
-    spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4)}[name]()
+    spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4),
+            "small7": lambda: scenes.small_random(7, n_tri=600, half=0.05)}[name]()
     cam = scenes.make_camera(*wh)
     blend = opt.get("blend")
     cfg = scenes.make_config(refmax, col_weight=blend if blend else 1.0)

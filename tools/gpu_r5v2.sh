@@ -1,0 +1,8 @@
+set -u
+OUT=gpurun_out/r5_v2
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu tests/test_shadow_rays.py tests/test_host_stream.py tests/test_js_dropin.py -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1 || exit $?
+timeout -k 10 300 python3 bench.py --config config3 --lights 2 --no-js --cpu-budget 0 --no-profile > $OUT/bench_config3_lights2.log 2>&1 || exit $?
+RT_SHADOW_CELLS=0 timeout -k 10 300 python3 bench.py --config config3 --lights 2 --no-js --cpu-budget 0 --no-profile > $OUT/bench_config3_lights2_tree.log 2>&1 || exit $?
+timeout -k 10 400 python3 bench.py --config config5 --lights 2 --no-js --cpu-budget 0 --no-profile > $OUT/bench_config5_lights2.log 2>&1 || exit $?
