@@ -82,7 +82,7 @@ struct RtDevice {
     hipStream_t stream = nullptr;
     RtDevScene scene{};
     DevBuf b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters,
-        b_fault, b_lights, b_shadow, b_sh, b_sh_tmp, b_sh_ints, b_gr[4];
+        b_fault, b_lights, b_shadow, b_shadow_f, b_sh, b_sh_tmp, b_sh_ints, b_gr[4];
     uint64_t lights_seq = 0;                     // the rt_set_lights call b_lights holds
     uint64_t sh_epoch = 0;                       // the scene (store epoch) b_sh's shadow tree was built for
     std::vector<std::array<hipEvent_t, 2>> ev;   // trace-kernel timing ring
@@ -757,8 +757,10 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
             L.ovf = L.queue[1] + P;
             // shadow rays: matte ends are deferred to k_shadow (at most one per ray)
             if (c->n_lights) {
-                if (d.b_shadow.ensure(sizeof(RtShadowRec) * (size_t)P) == RT_OK) {
+                if (d.b_shadow.ensure(sizeof(RtShadowRec) * (size_t)P) == RT_OK &&
+                    d.b_shadow_f.ensure(sizeof(double) * (size_t)c->n_lights * (size_t)P) == RT_OK) {
                     L.shadow_q = (RtShadowRec *)d.b_shadow.p;
+                    L.shadow_k = (double *)d.b_shadow_f.p;
                 } else {
                     (void)hipGetLastError();
                     L.cand = nullptr;                   // the fused kernel runs the frame

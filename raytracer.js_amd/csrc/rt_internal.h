@@ -279,11 +279,16 @@ struct RtLaunch {
     const rt_light *lights;
     RtShadowRec *shadow_q;                      // split path with lights: [rows*W] deferred matte ends
                                                 // (count ctr[2], k_shadow's claim head ctr[3]), else null
+    double *shadow_k;                           // [n_lights][rows*W]: light l's cosine * isl at record q, -1
+                                                // when it is skipped or blocked (k_shadow_rays; k_shadow
+                                                // adds rgb_l * k in light order)
 };
 
-// ctr: [0] overflow count, [1] its claim head, [2] deferred matte ends (shadow rays), [3] k_shadow's
-// claim head; a block of RT_CTR_LEVEL per bounce level from 4
-enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_INTS = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1) };
+// ctr: [0] overflow count, [1] its claim head, [2] deferred matte ends (shadow rays), [3] unused; a
+// block of RT_CTR_LEVEL per bounce level from 4; then k_shadow_rays' 8 claim heads, 32 ints apart (one
+// cache line each)
+enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_SH = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1),
+       RT_CTR_INTS = RT_CTR_SH + 8 * 32 };
 
 // walk_wait / walk_done (host-frame bands): the level-0 walk pass waits for event walk_wait (the
 // previous band's level-0 walk) and walk_done is recorded after it, so bands' walks run in order.

@@ -1327,56 +1327,95 @@ __device__ __forceinline__ bool shadow_blocked_tree(const RtDevScene &S, const R
 __device__ __forceinline__ bool shadow_blocked_grid(const RtDevScene &S, const RayBox &rb, float tlim,
                                                  const double q[3], const double u[3], double lim)
 {
-    for (int b = 0; b < S.g_nbig; b++) {
-        const RtBvh e = S.g_big[b];
-        if (ray_box_seg(e.lo, e.hi, rb, tlim) && prim_blocks(S, e.info, q, u, lim)) return true;
-    }
     const int res = S.g_res;
-    const float cs = S.g_cs, ext = cs * (float)res;
-    const float o[3] = {rb.ox, rb.oy, rb.oz}, iv[3] = {rb.ix, rb.iy, rb.iz};
-    const float uf[3] = {(float)u[0], (float)u[1], (float)u[2]};
-    float t0 = 0.0f, t1 = tlim;
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        const float ta = (S.g_lo[a] - o[a]) * iv[a], tb = (S.g_lo[a] + ext - o[a]) * iv[a];
-        t0 = fmaxf(t0, fminf(ta, tb));
-        t1 = fminf(t1, fmaxf(ta, tb));
-    }
-    if (!(t0 <= t1)) return false;
-    int c[3], stp[3];
-    float tm[3];
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        const float f = floorf((o[a] + uf[a] * t0 - S.g_lo[a]) / cs);
-        c[a] = f < 0.0f ? 0 : (f >= (float)res ? res - 1 : (int)f);
-        stp[a] = uf[a] > 0.0f ? 1 : (uf[a] < 0.0f ? -1 : 0);
-        tm[a] = stp[a] == 0 ? INFINITY : ((float)(c[a] + (stp[a] > 0)) * cs + S.g_lo[a] - o[a]) * iv[a];
-    }
-    uint32_t r = 0, re = 0;
-    bool load = true;
+    const float cs = S.g_cs;
+    // one loop of two paths, so that lanes at different points of their searches share trips: test the
+    // next entry (the large list's, then the current cell's), or go on to the next cell and load its
+    // range.  The DDA's state per axis lives in scalars, updated by selects (no divergent branch per
+    // axis, no scratch array): cell, step, next boundary parameter.
+    const RtBvh *arr = S.g_big;
+    uint32_t r = 0, re = (uint32_t)S.g_nbig;
+    bool started = false;
+    int c0 = 0, c1 = 0, c2 = 0, s0 = 0, s1 = 0, s2 = 0;
+    float m0 = 0, m1 = 0, m2 = 0, t1 = tlim;
     for (;;) {
         if (r < re) {
-            const RtBvh e = S.g_ref[r++];
+            const RtBvh e = arr[r++];
             if (ray_box_seg(e.lo, e.hi, rb, tlim) && prim_blocks(S, e.info, q, u, lim)) return true;
-        } else if (load) {
-            const uint32_t cell = ((uint32_t)c[2] * (uint32_t)res + (uint32_t)c[1]) * (uint32_t)res + (uint32_t)c[0];
-            r = S.g_cell[cell];
-            re = S.g_cell[cell + 1];
-            load = false;
-        } else {
-            const int a = tm[0] <= tm[1] ? (tm[0] <= tm[2] ? 0 : 2) : (tm[1] <= tm[2] ? 1 : 2);
-            if (!(tm[a] <= t1)) return false;                    // the segment ends in this cell
-            c[a] += stp[a];
-            if ((unsigned)c[a] >= (unsigned)res) return false;   // it leaves the grid
-            tm[a] = ((float)(c[a] + (stp[a] > 0)) * cs + S.g_lo[a] - o[a]) * iv[a];
-            load = true;
+            continue;
         }
+        if (!started) {
+            // clip the segment to the grid, and the cell it starts in
+            started = true;
+            const float o[3] = {rb.ox, rb.oy, rb.oz}, iv[3] = {rb.ix, rb.iy, rb.iz};
+            const float ext = cs * (float)res;
+            float t0 = 0.0f;
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const float ta = (S.g_lo[a] - o[a]) * iv[a], tb = (S.g_lo[a] + ext - o[a]) * iv[a];
+                t0 = fmaxf(t0, fminf(ta, tb));
+                t1 = fminf(t1, fmaxf(ta, tb));
+            }
+            if (!(t0 <= t1)) return false;
+            int cc[3], ss[3];
+            float mm[3];
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const float uf = (float)u[a];
+                const float f = floorf((o[a] + uf * t0 - S.g_lo[a]) / cs);
+                cc[a] = f < 0.0f ? 0 : (f >= (float)res ? res - 1 : (int)f);
+                ss[a] = uf > 0.0f ? 1 : (uf < 0.0f ? -1 : 0);
+                mm[a] = ss[a] == 0 ? INFINITY : ((float)(cc[a] + (ss[a] > 0)) * cs + S.g_lo[a] - o[a]) * iv[a];
+            }
+            c0 = cc[0]; c1 = cc[1]; c2 = cc[2];
+            s0 = ss[0]; s1 = ss[1]; s2 = ss[2];
+            m0 = mm[0]; m1 = mm[1]; m2 = mm[2];
+            arr = S.g_ref;
+        } else {
+            // the axis whose cell boundary comes first
+            const bool x = m0 <= m1 && m0 <= m2, y = !x && m1 <= m2;
+            const float ma = x ? m0 : (y ? m1 : m2);
+            if (!(ma <= t1)) return false;                       // the segment ends in this cell
+            const int sa = x ? s0 : (y ? s1 : s2);
+            const int ca = (x ? c0 : (y ? c1 : c2)) + sa;
+            if ((unsigned)ca >= (unsigned)res) return false;     // it leaves the grid
+            const float loa = x ? S.g_lo[0] : (y ? S.g_lo[1] : S.g_lo[2]);
+            const float oa = x ? rb.ox : (y ? rb.oy : rb.oz), iva = x ? rb.ix : (y ? rb.iy : rb.iz);
+            const float mn = ((float)(ca + (sa > 0)) * cs + loa - oa) * iva;
+            c0 = x ? ca : c0; c1 = y ? ca : c1; c2 = (!x && !y) ? ca : c2;
+            m0 = x ? mn : m0; m1 = y ? mn : m1; m2 = (!x && !y) ? mn : m2;
+        }
+        const uint32_t cell = ((uint32_t)c2 * (uint32_t)res + (uint32_t)c1) * (uint32_t)res + (uint32_t)c0;
+        r = S.g_cell[cell];
+        re = S.g_cell[cell + 1];
     }
 }
 
-// The shadow ray from q along u (unit) toward a light at distance dist (from the hit point, q being
-// 1e-3 along u from it): the grid search, or the tree search where no grid was built; culling off (or
-// a ray the f32 boxes cannot serve: rb.ok) tests every entity.
+// Every entity tested (the tree's records, every cull record, every leaf): for rays the f32 boxes
+// cannot serve, in the grid kernel (a small loop; out of line, the call's frame cost scratch).
+__device__ __forceinline__ bool shadow_blocked_all(const RtShNode *sh, int n_sh, const RtBvh *bvh, const RtPrim *prim,
+                                                const rt_shade *shades, double q0, double q1, double q2, double u0,
+                                                double u1, double u2, double lim)
+{
+    const double q[3] = {q0, q1, q2}, u[3] = {u0, u1, u2};
+    for (int k = 0; k < n_sh; k++) {
+        for (int i = sh[k].root; i >= 0;) {
+            const RtBvh b = bvh[i];
+            if (b.info < 0) { i++; continue; }
+            for (int slot = b.info >> 4; slot < (b.info >> 4) + (b.info & 15); slot++) {
+                Hit h;
+                if (prim_hit(prim[slot], q, u, h) == 0 || shades[prim[slot].meta >> 2].light) continue;
+                const double a = h.p[0] - q[0], c = h.p[1] - q[1], e = h.p[2] - q[2];
+                if (sqrt(dot3(a, c, e, a, c, e)) < lim) return true;
+            }
+            i = b.skip;
+        }
+    }
+    return false;
+}
+
+// GRID_ONLY: the caller knows the scene has a grid and culling is on (k_shadow's grid instantiation)
+template <bool GRID_ONLY = false>
 __device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, const double q[3], const double u[3],
                                             double dist)
 {
@@ -1385,6 +1424,10 @@ __device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, c
     float tlim = (float)(dist * 1.0001);
     if (!(tlim >= 0.0f)) tlim = INFINITY;
     const double lim = dist - 1e-3;
+    if (GRID_ONLY) {
+        if (rb.ok) return shadow_blocked_grid(S, rb, tlim, q, u, lim);
+        return shadow_blocked_all(S.shnode, S.n_sh, S.bvh, S.prim, S.shades, q[0], q[1], q[2], u[0], u[1], u[2], lim);
+    }
     if (prune && S.g_res > 0) return shadow_blocked_grid(S, rb, tlim, q, u, lim);
     return shadow_blocked_tree(S, rb, prune, tlim, q, u, lim);
 }
@@ -1419,6 +1462,7 @@ __device__ __forceinline__ void shadow_add(const RtLaunch &L, const rt_light &lt
 
 // The matte hit's light factor s (per channel): ambient + the unblocked lights' rgb * cosine * isl
 // (the fused kernels inline; the split path's k_shadow per deferred record).
+template <bool GRID_ONLY = false>
 __device__ __forceinline__ void shadow_factor(const RtDevScene &S, const RtLaunch &L, bool cull, const double p[3],
                                               const double nrm[3], double path, double s[3])
 {
@@ -1427,7 +1471,7 @@ __device__ __forceinline__ void shadow_factor(const RtDevScene &S, const RtLaunc
         const rt_light lt = L.lights[l];
         double q[3], u[3], dist, cosine;
         if (!shadow_ray(lt, p, nrm, q, u, dist, cosine)) continue;
-        if (shadow_blocked(S, cull, q, u, dist)) continue;
+        if (shadow_blocked<GRID_ONLY>(S, cull, q, u, dist)) continue;
         shadow_add(L, lt, path, dist, cosine, s);
     }
 }
@@ -1713,7 +1757,7 @@ __device__ __forceinline__ int32_t *pass_heads(const RtLaunch &L, int lv, int p)
 // set; an XCD whose band is done steals from the others.  The XCD is read from HW_REG_XCC_ID (gfx950
 // dispatches workgroups round-robin, but the register is authoritative).  Returns the first item
 // of a run of up to n in one band, *end = one past its last; items when everything is claimed.
-__device__ __forceinline__ int claim_xcd(int32_t *heads, int items, int lane, int n, int &end, bool xcd)
+__device__ __forceinline__ int claim_xcd(int32_t *heads, int items, int lane, int n, int &end, bool xcd, int hs = 1)
 {
     int t = items, e = items;
     if (!xcd) {                                   // one queue over all items
@@ -1729,8 +1773,8 @@ __device__ __forceinline__ int claim_xcd(int32_t *heads, int items, int lane, in
         for (int k = 0; k < 8; k++) {
             const int y = (x + k) & 7;
             const int lo = (int)((long long)items * y >> 3), size = (int)((long long)items * (y + 1) >> 3) - lo;
-            if (__hip_atomic_load(&heads[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= size) continue;
-            const int u = atomicAdd(&heads[y], n);
+            if (__hip_atomic_load(&heads[y * hs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= size) continue;
+            const int u = atomicAdd(&heads[y * hs], n);
             if (u < size) {
                 t = lo + u;
                 e = lo + (u + n < size ? u + n : size);
@@ -2393,9 +2437,19 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
     const bool queued = L.level == 0;             // level 0: the rays k_first queued
     const int n_q = queued ? *shade_n(L) : 0;
     const int n_it = queued ? (n_q + 63) >> 6 : items;
+    // level 0's queue (with lights: every primary ray, ~30 k items at 1080p) is dealt out by wave: its
+    // grid from the hints has about two waves per item, and a claim each serialised on one atomic
+    const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)), waves = (int)(gridDim.x * (blockDim.x >> 6));
+    int next = wave;
     for (;;) {
-        int t_end;
-        const int t0 = claim_xcd(pass_heads(L, L.level, 3), n_it, lane, ch, t_end, L.xcd_mask & 4);
+        int t_end, t0;
+        if (queued) {
+            t0 = next;
+            t_end = t0 + 1;
+            next += waves;
+        } else {
+            t0 = claim_xcd(pass_heads(L, L.level, 3), n_it, lane, ch, t_end, L.xcd_mask & 4);
+        }
         if (t0 >= n_it) break;
         for (int t = t0; t < t_end; t++) {
         RaySrc src;
@@ -2443,23 +2497,67 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
 }
 
 // Shadow rays on the split path (rt_set_lights): the matte ends the frame's passes
-// deferred (L.shadow_q, count ctr[2]), one lane per record: each light's shadow ray searched in the
-// shadow tree (shadow_blocked), the unblocked lights' terms added in light order, the pixel written.
+// deferred (L.shadow_q, count ctr[2]).  k_shadow_rays takes one (light, record) pair per lane, light
+// by light (64 consecutive records toward one light per wave: neighbouring pixels, coherent searches)
+// and writes the light's k = cosine * isl for the record (-1: skipped or blocked); k_shadow then adds
+// rgb_l * k in light order (shadow_add's operations) and writes the pixels.  A lane carries one search
+// and nothing of its record's colour.
+// GRID: the scene has a grid and culling is on (the host's choice; every other case runs GRID = false)
+template <int MINW, bool GRID>
+__global__ void __launch_bounds__(256, MINW) k_shadow_rays(RtLaunch L)
+{
+    TL_SCOPE(L.tl);
+    const int lane = threadIdx.x & 63;
+    const int n = L.ctr[2], nl = L.n_lights;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    const long long items = (long long)n * nl;
+    const int n_it = (int)((items + 63) >> 6);
+    const bool cull = L.cull != 0;
+    for (;;) {
+        // one item per claim from the wave's XCD's band of the items (8 heads on their own cache lines:
+        // one head would serialise ~60 k returning atomics), stealing from the others' when done
+        int t_end;
+        const int t0 = claim_xcd(L.ctr + RT_CTR_SH, n_it, lane, 1, t_end, true, 32);
+        if (t0 >= n_it) break;
+        for (int t = t0; t < t_end; t++) {
+        const long long it = (long long)t * 64 + lane;
+        if (it >= items) continue;
+        const int l = (int)(it / n), q = (int)(it - (long long)l * n);
+        const RtShadowRec &e = L.shadow_q[q];
+        const double p[3] = {e.p[0], e.p[1], e.p[2]}, nrm[3] = {e.n[0], e.n[1], e.n[2]};
+        double o[3], d[3], dist, cosine, k = -1.0;             // -1: the light is skipped or blocked
+        if (shadow_ray(L.lights[l], p, nrm, o, d, dist, cosine) && !shadow_blocked<GRID>(L.scene, cull, o, d, dist)) {
+            const double t = (e.path + dist) * L.cfg.distance_attenuation_factor;     // shadow_add's k
+            const double isl = 1.0 / (2.220446049250313e-16 + t * t);
+            k = cosine * isl;
+        }
+        L.shadow_k[(size_t)l * stride + (size_t)q] = k;
+        }
+    }
+}
+
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_shadow(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
     const int n = L.ctr[2];
-    const bool cull = L.cull != 0;
-    for (;;) {
-        const int base = claim(L.ctr + 3, lane) * 64;
-        if (base >= n) break;
+    const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
+    // uniform work: the records dealt out by wave, no claims
+    const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)), waves = (int)(gridDim.x * (blockDim.x >> 6));
+    for (int base = wave * 64; base < n; base += waves * 64) {
         const int q = base + lane;
         if (q >= n) continue;
-        const RtShadowRec e = L.shadow_q[q];
-        double s[3];
-        shadow_factor(L.scene, L, cull, e.p, e.n, e.path, s);
+        const RtShadowRec &e = L.shadow_q[q];
+        double s[3] = {L.ambient, L.ambient, L.ambient};
+        for (int l = 0; l < L.n_lights; l++) {
+            const double k = L.shadow_k[(size_t)l * stride + (size_t)q];
+            if (k < 0) continue;                               // skipped or blocked (a reaching k is >= 0 or NaN)
+            const rt_light lt = L.lights[l];
+            s[0] += lt.rgb[0] * k;
+            s[1] += lt.rgb[1] * k;
+            s[2] += lt.rgb[2] * k;
+        }
         RayResult R;
         R.rgb[0] = e.col[0] * s[0]; R.rgb[1] = e.col[1] * s[1]; R.rgb[2] = e.col[2] * s[2];
         R.hit_ent = e.hit_ent;
@@ -2961,7 +3059,15 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
         launch_persistent(k_cont<3>, st, Lc,
                           cont_hint == 0 && RT_NO_OP_BLOCKS > 0 && L.lv_blocks <= 0 ? RT_NO_OP_BLOCKS : level_blocks(L, cont_hint));
         // shadow rays (rt_set_lights): the deferred matte ends, after every pass that defers them
-        if (L.shadow_q) launch_persistent(k_shadow<4>, st, Lc);
+        if (L.shadow_q) {
+            // (RT_SHADOW_OCC: the grid kernel's waves per SIMD, 4 / 5 / 6)
+            static const int occ = getenv("RT_SHADOW_OCC") ? atoi(getenv("RT_SHADOW_OCC")) : 5;
+            if (L.cull && L.scene.g_res > 0)
+                launch_persistent(occ >= 6 ? k_shadow_rays<6, true> : (occ <= 4 ? k_shadow_rays<4, true> : k_shadow_rays<5, true>),
+                                  st, Lc);
+            else launch_persistent(k_shadow_rays<4, false>, st, Lc);
+            launch_persistent(k_shadow<8>, st, Lc);
+        }
         // this frame's counters come back for the next frames' grid hints (any recent frame will do)
         if (L.ctr_out) {
             HIP_TRY(hipMemcpyAsync(L.ctr_out, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
@@ -3114,7 +3220,9 @@ extern "C" int rt_debug_timeline(int32_t max, unsigned long long *rec4, char *na
             {(const void *)k_first<4>, "k_first"}, {(const void *)k_first<6>, "k_first"}, {(const void *)k_first<8>, "k_first"},
 
             {(const void *)k_shade<3>, "k_shade"}, {(const void *)k_shade<4>, "k_shade"}, {(const void *)k_shade<5>, "k_shade"},
-            {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow<4>, "k_shadow"}};
+            {(const void *)k_cont<3>, "k_cont"}, {(const void *)k_shadow_rays<6, true>, "k_shadow_rays"},
+            {(const void *)k_shadow_rays<5, true>, "k_shadow_rays"}, {(const void *)k_shadow_rays<4, true>, "k_shadow_rays"},
+            {(const void *)k_shadow_rays<4, false>, "k_shadow_rays"}, {(const void *)k_shadow<8>, "k_shadow"}};
         for (int i = 0; i < n; i++) {
             for (int q = 0; q < 4; q++) rec4[4 * i + q] = v[4 * i + q];
             const char *nm = "?";
