@@ -114,7 +114,7 @@ struct rt_ctx {
     int cand_cap = 64;               // candidate nodes per pixel in the split path (RT_CAND_CAP)
     int split_levels = RT_MAX_LEVELS + 1;   // split-path bounce levels (RT_SPLIT_LEVELS)
     int claim_chunk = 1;             // items per queue claim in the short passes (RT_CLAIM_CHUNK)
-    int xcd_mask = 0;                // passes claiming per-XCD bands (RT_XCD: 1 walk, 2 first, 4 shade)
+    int xcd_mask = 1;                // passes claiming per-XCD bands (RT_XCD: 1 walk, 2 first, 4 shade)
     int shade_occ = 3;               // k_shade occupancy variant (RT_SHADE_OCC)
     int cont_group = 8;              // continuation rays per wave (RT_CONT_GROUP, a power of two <= 64):
                                      // their passes are latency-bound, fewer lanes per wave shorten the

@@ -286,9 +286,9 @@ struct RtLaunch {
 
 // ctr: [0] overflow count, [1] its claim head, [2] deferred matte ends (shadow rays), [3] unused; a
 // block of RT_CTR_LEVEL per bounce level from 4; then k_shadow_rays' 8 claim heads, 32 ints apart (one
-// cache line each)
+// cache line each), and k_walk_first's per-XCD heads (RT_XCD bit 0) the same way
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_SH = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1),
-       RT_CTR_INTS = RT_CTR_SH + 8 * 32 };
+       RT_CTR_XW = RT_CTR_SH + 8 * 32, RT_CTR_INTS = RT_CTR_XW + 8 * 32 };
 
 // walk_wait / walk_done (host-frame bands): the level-0 walk pass waits for event walk_wait (the
 // previous band's level-0 walk) and walk_done is recorded after it, so bands' walks run in order.

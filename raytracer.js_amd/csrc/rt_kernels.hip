@@ -2373,13 +2373,16 @@ __global__ void __launch_bounds__(BS, MINW) k_walk_first(RtLaunch L)
     int32_t *head = pass_heads(L, L.level, 1);
     if (L.l0_half == 1) items = L.l0_split_tile;
     if (L.l0_half == 2) { t_base = L.l0_split_tile; items -= t_base; head += 1; }
+    // per-XCD bands (RT_XCD bit 0): 8 heads on their own cache lines (RT_CTR_XW)
+    const bool bands = (L.xcd_mask & 1) && !L.l0_half;
+    if (bands) head = L.ctr + RT_CTR_XW;
     const RtFrameSetup F = *L.setup;
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (;;) {
         int t_end;
-        int t = claim_xcd(head, items, lane, 1, t_end, (L.xcd_mask & 1) && !L.l0_half);
+        int t = claim_xcd(head, items, lane, 1, t_end, bands, 32);
         if (t >= items) break;
         t += t_base;
         RaySrc src;
