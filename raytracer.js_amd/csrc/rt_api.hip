@@ -91,7 +91,7 @@ struct RtDevice {
     // grid hints (rt_kernels.hip level_blocks): each frame copies its work counters back into one of
     // two pinned buffers (ctr_w) and records ctr_ev; the host reads only a copy whose event is done,
     // into ctr_snap, so launches never read a buffer a transfer may still be writing
-    int32_t *h_ctr = nullptr;                    // pinned: 2 x RT_CTR_INTS
+    int32_t *h_ctr = nullptr;                    // pinned: 2 x RT_CTR_HOST
     hipEvent_t ctr_ev[2] = {};
     bool ctr_pend[2] = {};
     uint64_t ctr_seq[2] = {}, ctr_snap_seq = 0, ctr_frames = 0;
@@ -125,6 +125,7 @@ struct rt_ctx {
     int refill = 16;                 // wide bounce levels walked with per-lane refill (RT_REFILL; 0: off)
     bool refill_always = false;      // RT_REFILL_ALWAYS=1: also levels no recent frame showed wide (tests)
     int seg_max = 64 * 4096;         // bounce levels of more rays run unsegmented, refilled (RT_SEG_MAX; 0: no limit)
+    int seg_lanes = 1 << 16;         // segments per ray doubled while a level's segments fit this many lanes (RT_SEG_LANES)
     bool hints = true;               // size bounce-level grids from a recent frame (RT_HINTS=0: full grids)
     int occ = 0;
     int diag = 0;
@@ -261,6 +262,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_REFILL")) c->refill = atoi(e) < 0 ? 0 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_REFILL_ALWAYS")) c->refill_always = atoi(e) != 0;
     if (const char *e = getenv("RT_SEG_MAX")) c->seg_max = atoi(e) < 0 ? 0 : atoi(e);
+    if (const char *e = getenv("RT_SEG_LANES")) c->seg_lanes = atoi(e) < 0 ? 0 : atoi(e);
     if (const char *e = getenv("RT_HINTS")) c->hints = atoi(e) != 0;
     if (const char *e = getenv("RT_OCC")) c->occ = atoi(e);
     if (const char *e = getenv("RT_DIAG")) c->diag = atoi(e);     // timing experiments only
@@ -632,8 +634,8 @@ static void fold_counts(RtDevice &d)
     for (int i = 0; i < 2; i++)
         if (d.ctr_pend[i] && hipEventQuery(d.ctr_ev[i]) == hipSuccess) {
             d.ctr_pend[i] = false;
-            if (d.ctr_seq[i] > d.ctr_snap_seq && d.h_ctr[(size_t)i * RT_CTR_INTS] >= 0) {
-                memcpy(d.ctr_snap.data(), d.h_ctr + (size_t)i * RT_CTR_INTS, sizeof(int32_t) * RT_CTR_INTS);
+            if (d.ctr_seq[i] > d.ctr_snap_seq && d.h_ctr[(size_t)i * RT_CTR_HOST] >= 0) {
+                memcpy(d.ctr_snap.data(), d.h_ctr + (size_t)i * RT_CTR_HOST, sizeof(int32_t) * RT_CTR_HOST);
                 d.ctr_snap_seq = d.ctr_seq[i];
             }
         }
@@ -674,12 +676,12 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.ctr = (int32_t *)d.b_ctr.p;
     if (c->hints) {
         if (!d.h_ctr) {
-            if (hipHostMalloc((void **)&d.h_ctr, 2 * sizeof(int32_t) * RT_CTR_INTS, hipHostMallocDefault) != hipSuccess ||
+            if (hipHostMalloc((void **)&d.h_ctr, 2 * sizeof(int32_t) * RT_CTR_HOST, hipHostMallocDefault) != hipSuccess ||
                 hipEventCreateWithFlags(&d.ctr_ev[0], hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&d.ctr_ev[1], hipEventDisableTiming) != hipSuccess)
                 return rt_set_error(RT_E_HIP, "prepare: grid-hint buffers");
-            d.ctr_snap.assign(RT_CTR_INTS, -1);                             // unknown until a frame completes
-            std::fill(d.h_ctr, d.h_ctr + 2 * RT_CTR_INTS, -1);
+            d.ctr_snap.assign(RT_CTR_HOST, -1);                             // unknown until a frame completes
+            std::fill(d.h_ctr, d.h_ctr + 2 * RT_CTR_HOST, -1);
         }
         fold_counts(d);
         // this frame's counters go to a buffer without a transfer in flight; with both busy (frames in
@@ -690,8 +692,8 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
             const int w = !d.ctr_pend[0] ? 0 : 1;
             d.ctr_pend[w] = true;
             d.ctr_seq[w] = ++d.ctr_frames;
-            d.h_ctr[(size_t)w * RT_CTR_INTS] = -1;                           // no transfer in flight to it
-            L.ctr_out = d.h_ctr + (size_t)w * RT_CTR_INTS;
+            d.h_ctr[(size_t)w * RT_CTR_HOST] = -1;                           // no transfer in flight to it
+            L.ctr_out = d.h_ctr + (size_t)w * RT_CTR_HOST;
             L.ctr_done = d.ctr_ev[w];
         }
     }
@@ -708,6 +710,7 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
     L.refill = c->refill;
     L.refill_always = c->refill_always;
     L.seg_max = c->seg_max;
+    L.seg_lanes = c->seg_lanes;
     L.walk_first = (int64_t)d.scene.n_list <= c->wf_list;
     L.l0_bs = c->l0_bs;
     L.shade_hint = c->shade_hint && c->hints;

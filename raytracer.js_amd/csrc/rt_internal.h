@@ -251,6 +251,7 @@ struct RtLaunch {
     int32_t refill;                             // wide bounce levels: idle lanes that take new rays (0: off; RT_REFILL)
     int32_t refill_always;                      // refill every wide level, not only where a recent frame had one (tests)
     int32_t seg_max;                            // bounce levels of more rays run unsegmented (0: no limit; RT_SEG_MAX)
+    int32_t seg_lanes;                          // narrow segmented levels: more segments per ray up to this many lanes (RT_SEG_LANES)
     int32_t walk_first;                         // level 0 as one walk + first-hit kernel (k_walk_first; §5.18)
     int32_t tl;                                 // RT_TL builds: this launch's timeline record (-1: none)
     int32_t l0_bs;                              // threads per block of k_walk_first (RT_L0_BS: 64 or 256)
@@ -286,9 +287,11 @@ struct RtLaunch {
 
 // ctr: [0] overflow count, [1] its claim head, [2] deferred matte ends (shadow rays), [3] unused; a
 // block of RT_CTR_LEVEL per bounce level from 4; then k_shadow_rays' 8 claim heads, 32 ints apart (one
-// cache line each), and k_walk_first's per-XCD heads (RT_XCD bit 0) the same way
+// cache line each).  The first RT_CTR_HOST ints come back to the host after a frame (grid hints).
+// Then per level the walk pass's 8 per-XCD claim heads, one cache line each (k_walk_first with
+// RT_XCD bit 0, k_walk_refill).
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_SH = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1),
-       RT_CTR_XW = RT_CTR_SH + 8 * 32, RT_CTR_INTS = RT_CTR_XW + 8 * 32 };
+       RT_CTR_XW = RT_CTR_SH + 8 * 32, RT_CTR_HOST = RT_CTR_XW, RT_CTR_INTS = RT_CTR_XW + 256 * (RT_MAX_LEVELS + 1) };
 
 // walk_wait / walk_done (host-frame bands): the level-0 walk pass waits for event walk_wait (the
 // previous band's level-0 walk) and walk_done is recorded after it, so bands' walks run in order.

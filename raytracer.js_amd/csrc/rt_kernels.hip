@@ -113,13 +113,25 @@ __device__ __forceinline__ uint32_t cand_off(const RtLaunch &, int k, uint32_t s
 {
     return ((uint32_t)k * stride + ray) << 2;
 }
+#ifndef RT_CAND_NT
+#define RT_CAND_NT 0
+#endif
 __device__ __forceinline__ void cand_store(const RtLaunch &L, int k, uint32_t stride, uint32_t ray, int node)
 {
-    *reinterpret_cast<int32_t *>(reinterpret_cast<char *>(L.cand) + cand_off(L, k, stride, ray)) = node;
+    int32_t *p = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(L.cand) + cand_off(L, k, stride, ray));
+#if RT_CAND_NT
+    __builtin_nontemporal_store(node, p);
+#else
+    *p = node;
+#endif
 }
 __device__ __forceinline__ int cand_load(const RtLaunch &L, int k, uint32_t stride, uint32_t ray)
 {
+#if RT_CAND_NT >= 2
+    return __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(L.cand) + cand_off(L, k, stride, ray)));
+#else
     return ld_at<int32_t>(L.cand, cand_off(L, k, stride, ray));
+#endif
 }
 
 // ---- Box.line_intersection (src/math/intersection.ts:150-204) on a cube ----------------------------
@@ -1752,6 +1764,11 @@ __device__ __forceinline__ int32_t *lvl_ctr(const RtLaunch &L, int lv) { return 
 // The 8 per-XCD claim heads of pass p (1 walk, 2 first, 3 shade) at level lv.
 __device__ __forceinline__ int32_t *pass_heads(const RtLaunch &L, int lv, int p) { return lvl_ctr(L, lv) + 8 * p; }
 
+// Level lv's walk-pass heads on separate cache lines (claim_xcd with hs = 32): a wave claims with a
+// returning atomic, and those on one line serialise (~15 ns each), which several thousand waves
+// starting at once, or refill claims every few trips, turn into a queue.
+__device__ __forceinline__ int32_t *walk_heads(const RtLaunch &L, int lv) { return L.ctr + RT_CTR_XW + 256 * lv; }
+
 // XCD-aware work claim.  Each XCD (its own 4 MB L2) owns one contiguous eighth of the items —
 // a horizontal band of the frame at level 0 — so the rays sharing an L2 share their scene working
 // set; an XCD whose band is done steals from the others.  The XCD is read from HW_REG_XCC_ID (gfx950
@@ -1947,7 +1964,7 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
 // holds the first hit.  A segment that ends without reaching the next seat (walk end, throw, step
 // cap) ends the ray there, and later segments are ignored.  The concatenated lists therefore give
 // the reference's first hit (or end) exactly, whatever seats floating point produces.
-// segments per ray: L.seg (a power of two <= 64), default 8
+// segments per ray: seg_k (L.seg, a power of two <= 64, default 8, more for narrow levels)
 enum : int { SEG_FIN = 0, SEG_THROW = 1, SEG_CAP = 2, SEG_SEATTHROW = 3, SEG_REACHED = 4, SEG_SKIP = 5 };
 
 __device__ __forceinline__ bool seg_mode(const RtLaunch &L)
@@ -1957,7 +1974,18 @@ __device__ __forceinline__ bool seg_mode(const RtLaunch &L)
            (long long)n * L.seg <= (long long)L.rows * (long long)L.cam.width;
 }
 
-// Segmented bounce levels: K = L.seg lanes per ray, lane = (ray lane / K,
+// Segments per ray of a segmented level: L.seg, doubled (up to 64) while the level's n rays stay
+// within L.seg_lanes lanes (RT_SEG_LANES) and their per-segment lists within the frame's P slots.  A
+// small part's level is a few thousand rays whose longest chain is the level's time (§7.1).
+__device__ __forceinline__ int seg_k(const RtLaunch &L)
+{
+    const long long n = *lvl_ctr(L, L.level - 1), P = (long long)L.rows * (long long)L.cam.width;
+    int K = L.seg;
+    while (K < 64 && n * K * 2 <= (long long)L.seg_lanes && n * K * 2 <= P) K *= 2;
+    return K;
+}
+
+// Segmented bounce levels: K = seg_k(L) lanes per ray, lane = (ray lane / K,
 // segment lane % K), 64 / K rays per work item; per-segment lists at index ray * K + segment.
 struct SegLane {
     int K, rpw, j, base, n_rays;
@@ -2132,7 +2160,7 @@ __global__ void __launch_bounds__(256, MINW) k_seg(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     if (!seg_mode(L) || seg_shaded(L) != SHADE) return;     // the other instantiation takes this level
-    seg_level<SHADE>(L, L.seg);
+    seg_level<SHADE>(L, seg_k(L));
 }
 
 // Walk pass of a wide bounce level with per-lane refill (RT_REFILL = G > 0; levels of 64 rays per
@@ -2146,6 +2174,8 @@ __device__ __forceinline__ bool refill_level(const RtLaunch &L)
     return L.refill > 0 && L.level >= 1 && !seg_mode(L) && cont_g(L) == 64;
 }
 
+// (Level 0 walked this way, ray r = lane r % 64 of tile r / 64, lost: config 5 43.9 -> 49.9 ms,
+// config 3 2.68 -> 3.15 ms against the tile-per-wave walk pass)
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
 {
@@ -2156,7 +2186,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const int n_rays = *lvl_ctr(L, L.level - 1);
-    int32_t *head = pass_heads(L, L.level, 1);
+    int32_t *heads = walk_heads(L, L.level);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Walker w;
     RayBox rb;
@@ -2167,12 +2197,13 @@ __global__ void __launch_bounds__(256, MINW) k_walk_refill(RtLaunch L)
         const unsigned long long m_walk = __ballot(res == 1);
         const int idle = 64 - __popcll(m_walk);
         if (!drained && (idle >= L.refill || !m_walk)) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(head, idle);
-            base = __builtin_amdgcn_readfirstlane(__shfl(base, 0, 64));
-            drained = base + idle >= n_rays;
+            // a run of up to `idle` rays from this XCD's band (then the others'): a short run at a
+            // band's end leaves some lanes idle until the next claim
+            int t_end;
+            const int base = claim_xcd(heads, n_rays, lane, idle, t_end, true, 32);
+            drained = base >= n_rays;
             const int r = base + __popcll(~m_walk & below);
-            if (res != 1 && r < n_rays) {
+            if (res != 1 && r < t_end) {
                 q = r;
                 n = 0;
                 const RtCont *rec = lvl_queue(L, L.level - 1) + q;
@@ -2373,9 +2404,9 @@ __global__ void __launch_bounds__(BS, MINW) k_walk_first(RtLaunch L)
     int32_t *head = pass_heads(L, L.level, 1);
     if (L.l0_half == 1) items = L.l0_split_tile;
     if (L.l0_half == 2) { t_base = L.l0_split_tile; items -= t_base; head += 1; }
-    // per-XCD bands (RT_XCD bit 0): 8 heads on their own cache lines (RT_CTR_XW)
+    // per-XCD bands (RT_XCD bit 0): 8 heads on their own cache lines
     const bool bands = (L.xcd_mask & 1) && !L.l0_half;
-    if (bands) head = L.ctr + RT_CTR_XW;
+    if (bands) head = walk_heads(L, 0);
     const RtFrameSetup F = *L.setup;
     const RtDevScene &S = L.scene;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
@@ -2816,7 +2847,7 @@ template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_level(RtLaunch L)
 {
     TL_SCOPE(L.tl);
-    seg_level<true>(L, seg_mode(L) ? L.seg : 1);
+    seg_level<true>(L, seg_mode(L) ? seg_k(L) : 1);
 }
 
 template <bool INCL_UNDEF>
@@ -3073,7 +3104,7 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
         }
         // this frame's counters come back for the next frames' grid hints (any recent frame will do)
         if (L.ctr_out) {
-            HIP_TRY(hipMemcpyAsync(L.ctr_out, L.ctr, sizeof(int32_t) * RT_CTR_INTS, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(L.ctr_out, L.ctr, sizeof(int32_t) * RT_CTR_HOST, hipMemcpyDeviceToHost, st));
             if (L.ctr_done) HIP_TRY(hipEventRecord((hipEvent_t)L.ctr_done, st));
         }
     }

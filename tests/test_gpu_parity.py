@@ -415,16 +415,19 @@ def _thin_mirrors(spec, every):
 # (scene, RT_CAND_CAP, segments per ray k, mirror thinning).  k = 32 needs bounce levels of at most
 # W*H/32 rays; the thinning factors were picked with the oracle so that every level fits (bounce
 # segments 180-308 against 2000 at 320x200, 259 against 512 at 128x128).
-SEG_CASES = [(n, cap, 8, 1) for n in ("config1", "small3", "small8", "transmission", "config2") for cap in (None, "2")] + \
-    [("small3", None, 32, 3), ("small8", None, 32, 4), ("transmission", None, 32, 3), ("config2", None, 32, 1),
-     ("small8", "2", 32, 4)]
+SEG_CASES = [(n, cap, 8, 1, "0") for n in ("config1", "small3", "small8", "transmission", "config2") for cap in (None, "2")] + \
+    [("small3", None, 32, 3, "0"), ("small8", None, 32, 4, "0"), ("transmission", None, 32, 3, "0"),
+     ("config2", None, 32, 1, "0"), ("small8", "2", 32, 4, "0")] + \
+    [(n, cap, 8, 1, lanes) for n, cap in (("config1", None), ("small8", "2"), ("transmission", None), ("config2", None))
+     for lanes in (None, "4194304")]
 
 
-@pytest.mark.parametrize("name,cap,k,thin", SEG_CASES)
-def test_segmented_equals_unsegmented(ctx, name, cap, k, thin, monkeypatch):
+@pytest.mark.parametrize("name,cap,k,thin,lanes", SEG_CASES)
+def test_segmented_equals_unsegmented(ctx, name, cap, k, thin, lanes, monkeypatch):
     """Segmented continuation walks (k lanes per bounce ray, each walking one
     stretch of its root crossing) change scheduling, not results: identical frames against RT_SEG=0
-    and the oracle at refmax 5, also when segment lists overflow (RT_CAND_CAP=2)."""
+    and the oracle at refmax 5, also when segment lists overflow (RT_CAND_CAP=2).  RT_SEG_LANES=0 keeps
+    k segments per ray; the default (2^16) and 2^22 let narrow levels double k up to 64 (seg_k)."""
     spec = {"config1": scenes.config1_spheres, "small3": lambda: scenes.small_random(3),
             "small8": lambda: scenes.small_random(8, n_tri=800, half=0.04),
             "transmission": _transmission_spec, "config2": scenes.config2}[name]()
@@ -435,6 +438,8 @@ def test_segmented_equals_unsegmented(ctx, name, cap, k, thin, monkeypatch):
     if cap:
         monkeypatch.setenv("RT_CAND_CAP", cap)
     monkeypatch.setenv("RT_SEG", str(k))
+    if lanes is not None:
+        monkeypatch.setenv("RT_SEG_LANES", lanes)
     ctxs = []
     try:
         seg = rtamd.Context(0)
