@@ -106,32 +106,21 @@ __device__ __forceinline__ int4 node_up4(const RtDevScene &S, int n) { return ld
 struct RayBox;
 __device__ __forceinline__ bool node_candidate(const RtDevScene &S, int n, bool cull, const RayBox &rb);
 
-// Candidate lists are k-major [cand_cap][rays] int32 (ray-major lists measured slower, §5.18);
+// Candidate lists are k-major [cand_cap][rays] int32 (ray-major lists measured slower, §5.18; so did
+// non-temporal list stores and loads, round 5);
 // cand_cap * rays * 4 < 2^32 is ensured by the host (prepare caps cand_cap), so the address is a
 // 32-bit offset from the uniform base.
 __device__ __forceinline__ uint32_t cand_off(const RtLaunch &, int k, uint32_t stride, uint32_t ray)
 {
     return ((uint32_t)k * stride + ray) << 2;
 }
-#ifndef RT_CAND_NT
-#define RT_CAND_NT 0
-#endif
 __device__ __forceinline__ void cand_store(const RtLaunch &L, int k, uint32_t stride, uint32_t ray, int node)
 {
-    int32_t *p = reinterpret_cast<int32_t *>(reinterpret_cast<char *>(L.cand) + cand_off(L, k, stride, ray));
-#if RT_CAND_NT
-    __builtin_nontemporal_store(node, p);
-#else
-    *p = node;
-#endif
+    *reinterpret_cast<int32_t *>(reinterpret_cast<char *>(L.cand) + cand_off(L, k, stride, ray)) = node;
 }
 __device__ __forceinline__ int cand_load(const RtLaunch &L, int k, uint32_t stride, uint32_t ray)
 {
-#if RT_CAND_NT >= 2
-    return __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(L.cand) + cand_off(L, k, stride, ray)));
-#else
     return ld_at<int32_t>(L.cand, cand_off(L, k, stride, ray));
-#endif
 }
 
 // ---- Box.line_intersection (src/math/intersection.ts:150-204) on a cube ----------------------------
