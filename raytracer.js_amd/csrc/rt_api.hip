@@ -188,8 +188,10 @@ static void release_device(RtDevice &d)
 {
     (void)hipSetDevice(d.device);
     for (DevBuf *b : {&d.b_cand, &d.b_cand_n, &d.b_first, &d.b_queue, &d.b_ctr, &d.b_setup, &d.b_dirs, &d.b_rgb,
-                      &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault, &d.b_lights, &d.b_shadow})
+                      &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault, &d.b_lights, &d.b_shadow,
+                      &d.b_shadow_f, &d.b_sh, &d.b_sh_tmp, &d.b_sh_ints})
         b->release();
+    for (DevBuf &b : d.b_gr) b.release();
     for (auto &e : d.ev)
         for (hipEvent_t x : e)
             if (x) (void)hipEventDestroy(x);

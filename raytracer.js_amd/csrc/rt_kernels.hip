@@ -196,10 +196,18 @@ __device__ int node_at_pos(const RtDevScene &S, const double p[3], int &tree, in
 // ---- OctreeWalker (src/octree_space.ts:159-408) ---------------------------------------------------
 enum : int { F_RET = 1, F_STEPPED = 2, F_AHEAD = 4 };
 
+// f32 reciprocal of a direction component, clamped away from 0: the cull hierarchy's ray (RayBox) and
+// the slot exit's screen (Walker::inv) share it
+__device__ __forceinline__ float safe_inv(double d)
+{
+    const double dd = fabs(d) < 1e-30 ? copysign(1e-30, d) : d;
+    return 1.0f / (float)dd;
+}
+
 struct Walker {
     double o[3], d[3];     // this.pos / this.direction
-    double inv[3];         // RN(1/d) per axis, for the slot-exit selection (see slot_exit)
-    bool fast;             // every d component is 0 or normal: the reciprocal shortcut is valid
+    float inv[3];          // safe_inv(d) per axis, for the slot-exit screen (see slot_exit)
+    bool fast;             // every |d| component in [1e-30, 1e30]: the reciprocal screen is valid
     double np[3];          // next_pos[0]
     int nn;                // next_pos[1]: face index | negate << 3 | valid << 4
     int cur_tree;          // -1: cur_node undefined
@@ -259,9 +267,10 @@ __device__ __forceinline__ int walker_set(const RtDevScene &S, Walker &w, const 
     bool fast = true;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        w.inv[a] = 1.0 / d[a];
-        // a subnormal component makes RN(1/d) overflow; a huge one underflows it
-        fast = fast && (d[a] == 0.0 || (fabs(d[a]) >= 2.2250738585072014e-308 && fabs(d[a]) <= 1e300) || isnan(d[a]));
+        w.inv[a] = safe_inv(d[a]);
+        // the screen's error bound needs a normal f32 reciprocal of a normal f32 component (0, NaN,
+        // tiny and huge components take the exact six divisions)
+        fast = fast && fabs(d[a]) >= 1e-30 && fabs(d[a]) <= 1e30;
     }
     w.fast = fast;
     return walker_setup(S, w) < 0 ? -1 : 0;
@@ -288,10 +297,12 @@ __device__ bool reseat_throws(const RtDevScene &S, const double p[3], const doub
 // The exit half of Box.line_intersection (src/math/intersection.ts:150-204) for a walker slot:
 // u2 = the first minimum over exit faces of q/p and the emptiness check u1 > u2, bit-identical to
 // six IEEE divisions.  Exactly one face per axis is an exit face (isNegative(p) selects entering),
-// so three exit and three entry quotients exist.  Each is first approximated by q * RN(1/d),
-// which is within 3 ulps of RN(q/d) (relative error <= 3 eps for normal d; exact for d = +-0
-// where both are +-inf or NaN).  Any candidate farther than 8 ulps from the minimum cannot be
-// (or tie with) the exact minimum, so only the survivors are divided exactly — normally one.
+// so three exit and three entry quotients exist.  Each is first approximated by q * r with
+// r = RN32(1/RN32(d)) (w.inv, w.fast: 1e-30 <= |d| <= 1e30), within relative 2^-23 + 2^-53 of q/d.
+// A candidate farther than |m| * 2^-21 above the minimum m of the approximations cannot be (or tie
+// with) the exact minimum (the true minimum's approximation exceeds m by at most ~2.4e-7 |m|), so
+// only the survivors are divided exactly — normally one.  (An f64 reciprocal with an 8-ulp screen
+// held 6 more VGPRs per walker; round 5.)
 // Returns false for the reference's [] (then update_next_pos throws).
 // The slot is given by its planes: tl[a] = the Box's `center - size*0.5` per axis (its lower face),
 // top[a] = `tl + size` (its upper face), computed with the reference's operations by the caller.
@@ -310,15 +321,16 @@ __device__ __forceinline__ bool slot_exit(const double tl[3], const double top[3
         // (neg ? -inv : inv) is |inv| (inv = RN(1/d) has d's sign; a NaN quotient never survives):
         // the abs / neg source modifiers of the multiply, no per-ray register copies
         qe[a] = neg ? qlo : qhi;
-        ae[a] = qe[a] * fabs(w.inv[a]);
-        const double an = (neg ? qhi : qlo) * -fabs(w.inv[a]);
+        const double ra = (double)fabsf(w.inv[a]);
+        ae[a] = qe[a] * ra;
+        const double an = (neg ? qhi : qlo) * -ra;
         M = an > M ? an : M;
     }
     // exit: the reference keeps the first strict minimum over faces in order (u2 starts at +inf)
     double m = INFINITY;
 #pragma unroll
     for (int a = 0; a < 3; a++) m = ae[a] < m ? ae[a] : m;
-    const double tol = fabs(m) * 1.7763568394002505e-15 + 1e-300;   // 8 eps |m| + subnormal slack
+    const double tol = fabs(m) * 4.76837158203125e-07 + 1e-300;   // 2^-21 |m| + subnormal slack
     const bool s0 = ae[0] <= m + tol, s1 = ae[1] <= m + tol, s2 = ae[2] <= m + tol;   // NaN never survives
     // the common case, straight-line: one survivor of a finite minimum in the shortcut's range,
     // selected without branching so that every lane of the wave shares one division
@@ -350,7 +362,7 @@ __device__ __forceinline__ bool slot_exit(const double tl[3], const double top[3
         }
     }
     // entry: only `u1 > u2` matters; divided exactly only when the screen cannot decide
-    const double tolM = fabs(M) * 1.7763568394002505e-15 + 1e-300;
+    const double tolM = fabs(M) * 4.76837158203125e-07 + 1e-300;
     if (M > -INFINITY && (!(M + tolM < u2) || !(fabs(M) < 1e300))) {
         double u1 = -INFINITY;
 #pragma unroll
@@ -834,12 +846,6 @@ struct RayBox {
     bool ok;           // finite ray: culling allowed
 };
 
-__device__ __forceinline__ float safe_inv(double d)
-{
-    const double dd = fabs(d) < 1e-30 ? copysign(1e-30, d) : d;
-    return 1.0f / (float)dd;
-}
-
 __device__ __forceinline__ RayBox make_raybox(const double o[3], const double d[3])
 {
     RayBox rb;
@@ -1258,10 +1264,10 @@ __device__ __forceinline__ RtCont *lvl_queue(const RtLaunch &L, int k)
 // A light is blocked when some entity of the scene that is not a light has a forward hit (or a
 // throwing test) nearer than dist - 1e-3 from the shadow ray's start: an existence question, so the
 // search may visit entities in any order and skip any it can prove cannot answer it.  It runs over the
-// shadow tree (RtShNode: the octree's non-empty subtrees in pre-order with their cull boxes' union),
-// then each visited node's own cull hierarchy, pruning boxes the segment [0, dist] misses, with the
-// exact binary64 test as the only decision: one flat loop (a trip is one tree record, one hierarchy
-// record or one exact test), like scan_first.
+// scene's uniform grid (shadow_blocked_grid), or without one over the shadow tree (RtShNode: the
+// octree's non-empty subtrees in pre-order with their cull boxes' union) and each visited node's own
+// cull hierarchy; boxes the segment [0, dist] misses are pruned, and the exact binary64 test is the
+// only decision.
 
 // The slab test of ray_box on the segment t in [0, tlim] (tlim: the light's distance rounded up).
 __device__ __forceinline__ bool ray_box_seg(const float *lo, const float *hi, const RayBox &rb, float tlim)
@@ -2282,7 +2288,8 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
 // a matte (REFLECTION, not a mirror) surface without an image texture and not at an acute normal.
 // The colour is trace_ray's for that case, in its operation order (col starts at 1: 1 * x == x; path
 // starts at +0).  Returns false for every other ray, which k_shade shades as before; a ray ended
-// here gets first = {-2, -2}.
+// here gets first = {-2, -2}.  With lights (L.shadow_q) a matte end is deferred to k_shadow with the
+// record trace_ray would push (R.status = ST_DEFER: no pixel write here).
 __device__ __forceinline__ bool early_shade(const RtLaunch &L, const RaySrc &src, int cn, int2 hit, RayResult &R)
 {
     const RtDevScene &S = L.scene;
@@ -2317,6 +2324,15 @@ __device__ __forceinline__ bool early_shade(const RtLaunch &L, const RaySrc &src
     }
     R.hit_ent = S.list_entity[pr.rank];
     R.hit_node = hit.x;
+    if (!sh.light && L.shadow_q) {
+        // the matte end with lights: trace_ray's path update and shadow_push at the hit point
+        const double a = h.p[0] - src.o[0], b = h.p[1] - src.o[1], e = h.p[2] - src.o[2];
+        double path = 0;
+        path += sqrt(dot3(a, b, e, a, b, e));
+        shadow_push(L, h.p, h.n, c0, c1, c2, path, R, src.pix);
+        R.status = ST_DEFER;
+        return true;
+    }
     R.rgb[0] = c0; R.rgb[1] = c1; R.rgb[2] = c2;
     return true;
 }
@@ -2343,10 +2359,10 @@ __device__ __forceinline__ void first_finish(const RtLaunch &L, const RaySrc &sr
         // level 0: end the plain terminal rays here; queue the rest for k_shade (ray_cn is free at
         // level 0), wave by wave so a shading wave keeps a tile's rays together
         RayResult R;
-        // (with lights a matte end is deferred to k_shadow: every ray goes to k_shade)
-        if (!(cn >= 0 && !fault && !L.shadow_q && early_shade(L, src, cn, res, R)))
+        // (with lights a matte end is deferred to k_shadow by early_shade: ST_DEFER)
+        if (!(cn >= 0 && !fault && early_shade(L, src, cn, res, R)))
             L.ray_cn[wave_reserve(shade_n(L))] = (int)src.id;
-        else write_pixel(L, (size_t)src.pix, R);
+        else if (R.status != ST_DEFER) write_pixel(L, (size_t)src.pix, R);
     }
     reinterpret_cast<int2 *>(L.first)[src.id] = res;
 }
@@ -3139,9 +3155,12 @@ int rt_launch_shadow_grid(RtDevScene *S, const int32_t *depth, int res, RtGridAl
     S->g_big = nullptr;
     const int N = S->n_nodes;
     if (N <= 0 || S->n_list <= 0) return RT_OK;
-    if (res <= 0) {                                   // about one primitive per cell, 8 .. 256 per axis
-        res = 8;
-        while (res < 256 && (double)res * res * res < (double)S->n_list) res *= 2;
+    if (res <= 0) {
+        // about one primitive per cell: the cube root of the list entries, up to a multiple of 8, 8 .. 256
+        // per axis (config 3 + 2 lights: 48 per axis 539.7 Mrays/s, 64: 530.4, 32: 514.8; config 5:
+        // 104, where 96 / 128 / 64 gave 227.8 / 229.0 / 221.4; profiles/r5_v17/)
+        res = (int)std::ceil(std::cbrt((double)S->n_list) / 8.0) * 8;
+        res = std::min(256, std::max(8, res));
     }
     res = std::min(512, std::max(2, res));
     RtNode root;
