@@ -114,7 +114,8 @@ struct rt_ctx {
     int cand_cap = 64;               // candidate nodes per pixel in the split path (RT_CAND_CAP)
     int split_levels = RT_MAX_LEVELS + 1;   // split-path bounce levels (RT_SPLIT_LEVELS)
     int claim_chunk = 1;             // items per queue claim in the short passes (RT_CLAIM_CHUNK)
-    int xcd_mask = 1;                // passes claiming per-XCD bands (RT_XCD: 1 walk, 2 first, 4 shade)
+    int xcd_mask = 1;                // passes claiming per-XCD bands (RT_XCD: 1 k_walk_first, 2 first, 4 shade,
+                                     // 8 the fused kernel, k_walk and the segmented levels)
     int shade_occ = 3;               // k_shade occupancy variant (RT_SHADE_OCC)
     int cont_group = 8;              // continuation rays per wave (RT_CONT_GROUP, a power of two <= 64):
                                      // their passes are latency-bound, fewer lanes per wave shorten the
@@ -253,7 +254,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_SPLIT")) c->split = atoi(e) != 0;
     if (c->flags & RT_CREATE_NO_SPLIT) c->split = false;
     if (const char *e = getenv("RT_CAND_CAP")) c->cand_cap = atoi(e) < 1 ? 1 : atoi(e);
-    if (const char *e = getenv("RT_XCD")) c->xcd_mask = atoi(e) & 7;
+    if (const char *e = getenv("RT_XCD")) c->xcd_mask = atoi(e) & 15;
     if (const char *e = getenv("RT_SHADE_OCC")) c->shade_occ = atoi(e);
     if (const char *e = getenv("RT_CLAIM_CHUNK")) c->claim_chunk = atoi(e) < 1 ? 1 : (atoi(e) > 64 ? 64 : atoi(e));
     if (const char *e = getenv("RT_SPLIT_LEVELS")) c->split_levels = atoi(e) < 1 ? 1 : atoi(e);

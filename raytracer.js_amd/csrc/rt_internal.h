@@ -242,7 +242,7 @@ struct RtLaunch {
     int32_t cont_group;                         // continuation rays per wave (levels >= 1)
     int32_t split_levels;                       // bounce levels on the split path; deeper ones run in k_cont
     int32_t claim_chunk;                        // work items per queue claim in k_first / k_shade
-    int32_t xcd_mask;                           // passes with per-XCD work bands: 1 walk, 2 first, 4 shade
+    int32_t xcd_mask;                           // per-XCD work bands: 1 k_walk_first, 2 first, 4 shade, 8 other walks
     int32_t shade_occ;                          // k_shade waves per SIMD the registers must admit (3, 4, 5)
     int32_t seg;                                // segments per bounce ray, levels >= 1 (0: off; RT_SEG; §5.10)
     int32_t *ray_cn;                            // device [rows*W]: per-ray status of a segmented level

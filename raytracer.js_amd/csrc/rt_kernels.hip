@@ -1898,7 +1898,7 @@ __global__ void __launch_bounds__(256, MINW) k_trace(RtLaunch L)
     const RayQueues Q = {nullptr, nullptr, nullptr, nullptr, false};
     for (;;) {
         int t_end;
-        const int t = claim_xcd(pass_heads(L, 0, 1), n_tiles, lane, 1, t_end, L.xcd_mask & 1);
+        const int t = claim_xcd(pass_heads(L, 0, 1), n_tiles, lane, 1, t_end, L.xcd_mask & 8);
         if (t >= n_tiles) break;
         const long long t_tile = (STATS && (L.diag & 8)) ? (long long)clock64() : 0;
         RaySrc src;
@@ -2128,7 +2128,7 @@ __device__ __forceinline__ void seg_level(const RtLaunch &L, int K)
     const int items = (g.n_rays + g.rpw - 1) / g.rpw;
     for (;;) {
         int t_end;
-        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
+        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 8);
         if (t >= items) break;
         const int cn = seg_walk_item(L, S, g, t, stride, c);
         int2 out;
@@ -2269,7 +2269,7 @@ __global__ void __launch_bounds__(256, MINW) k_walk(RtLaunch L)
     if (L.walk_first && L.level == 0) return;         // k_walk_first takes level 0
     for (;;) {
         int t_end;
-        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 1);
+        const int t = claim_xcd(pass_heads(L, L.level, 1), items, lane, 1, t_end, L.xcd_mask & 8);
         if (t >= items) break;
         RaySrc src;
         ray_src(L, t, lane, src);

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Per-kernel A/B over several builds of librt_amd.so on one box: rocprofv3 --kernel-trace over
 # tools/sweep.py for each LIBS entry (name=path; "cur" = the working tree's build), printing each
-# kernel's total time per frame.  Each GPU step has its own time limit; stops at the first failure.
+# kernel's total time per split-path frame (sweep.py traces FRAMES + 2 of them, and one counting frame
+# whose k_trace is listed apart; round 5 fixed a divisor of FRAMES + 3).  Each GPU step has its own time limit; stops at the first failure.
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/abl}
 FR=${FRAMES:-10}
@@ -12,7 +13,7 @@ for E in ${LIBS:-cur=}; do
   rm -rf "$OUT/$L"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/$L" -o kt --output-format csv -- \
       python3 tools/sweep.py --frames $FR ${SWEEP_ARGS:-} ${SWEEP:-base:} > "$OUT/$L.log" 2>&1 || { echo "$L failed"; tail -5 "$OUT/$L.log"; exit 1; }
-  python3 - "$OUT/$L" $((FR + 3)) $L <<'PY'
+  python3 - "$OUT/$L" $((FR + 2)) $L <<'PY'
 import csv, glob, sys, re
 d, frames, tag = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 tot = {}
