@@ -387,6 +387,36 @@ def test_walk_refill_equals_waves(ctx, name, refill, cap, monkeypatch):
     _compare(w.trace_frame(root, cam, cfg, nthreads=8), frames[1])
 
 
+@pytest.mark.parametrize("xcd", ["0", "15"])
+@pytest.mark.parametrize("name", ["small8", "transmission", "config2"])
+def test_xcd_bands_equal_default(ctx, name, xcd, monkeypatch):
+    """Per-XCD work bands (RT_XCD: 1 k_walk_first, the default; 2 first hit; 4 shading; 8 the fused
+    kernel, k_walk and the segmented levels; claim heads on their own cache lines for the walks) only
+    change which wave takes which work: frames equal the default's on the split and the fused paths,
+    two frames per context (the second with hints), at refmax 5 with segmented and overflowing levels."""
+    spec = {"small8": lambda: scenes.small_random(8, n_tri=800, half=0.04), "transmission": _transmission_spec,
+            "config2": scenes.config2}[name]()
+    cam, cfg = scenes.make_camera(203, 133), scenes.make_config(5)
+    scene = rtamd.build_scene(spec)
+    want = {}
+    for env in ({}, {"RT_XCD": xcd}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        for flags in (0, abi.RT_CREATE_NO_SPLIT):
+            c = rtamd.Context(0, flags=flags)
+            try:
+                c.upload(scene)
+                frames = [c.trace_frame(cam, cfg, stats=False, allow_fault=True) for _ in range(2)]
+            finally:
+                c.close()
+            _same_frames(frames[0], frames[1])
+            if flags not in want:
+                want[flags] = frames[0]
+            else:
+                _same_frames(want[flags], frames[0])
+    _same_frames(want[0], want[abi.RT_CREATE_NO_SPLIT])
+
+
 def _transmission_spec():
     spec = scenes.small_random(5)
     sh = spec.shades.copy()
