@@ -123,9 +123,9 @@ def test_walker_matches_oracle_random_rays(ctx):
 
 
 def test_walker_special_directions(ctx):
-    """Slot-exit shortcut (q * RN(1/d) screening, exact division for survivors) against the
-    oracle's six IEEE divisions: directions with +-0, subnormal, tiny and huge components, dyadic
-    origins on node boundaries (exact ties between exit faces)."""
+    """Slot-exit shortcut (q * RN32(1/RN32(d)) screening within 2^-21, exact division for survivors)
+    against the oracle's six IEEE divisions: directions with +-0, subnormal, tiny and huge components
+    (those take the exact path), dyadic origins on node boundaries (exact ties between exit faces)."""
     spec = scenes.small_random(9, n_tri=400, depth=6)
     ctx.upload(rtamd.build_scene(spec))
     w, root = oracle.build_scene(spec)
