@@ -82,9 +82,11 @@ struct RtDevice {
     hipStream_t stream = nullptr;
     RtDevScene scene{};
     DevBuf b_cand, b_cand_n, b_first, b_queue, b_ctr, b_setup, b_dirs, b_rgb, b_hit_e, b_hit_n, b_status, b_counters,
-        b_fault, b_lights, b_shadow, b_shadow_f, b_sh, b_sh_tmp, b_sh_ints, b_gr[4];
+        b_fault, b_lights, b_shadow, b_shadow_f, b_sh, b_sh_tmp, b_sh_ints, b_gr[4 + 4 * RT_MAX_LIGHTS], b_lmaps;
     uint64_t lights_seq = 0;                     // the rt_set_lights call b_lights holds
     uint64_t sh_epoch = 0;                       // the scene (store epoch) b_sh's shadow tree was built for
+    RtLightMap lmap[RT_MAX_LIGHTS] = {};         // the lights' direction maps (b_gr[4 + 4 l ..]; copied to b_lmaps)
+    uint64_t lm_epoch = 0, lm_seq = 0;           // the scene and light list they were built for
     std::vector<std::array<hipEvent_t, 2>> ev;   // trace-kernel timing ring
     int ev_next = 0, ev_count = 0;
     hipEvent_t sync = nullptr;                   // cross-stream / cross-device ordering
@@ -108,6 +110,8 @@ struct rt_ctx {
     int stream_gated = 0;            // host frames the streaming gate declined since dev[0]'s last count
     int shadow_grid = 0;             // shadow rays' grid cells per axis (RT_SHADOW_GRID; 0: from the primitive count,
                                      // -1: no grid, the tree search)
+    int light_map = 0;               // shadow rays' direction maps, cells per face axis (RT_LIGHT_MAP; 0: from the
+                                     // primitive count, -1: none, the grid search)
     double ambient = 0;
     rt_light lights[RT_MAX_LIGHTS] = {};
     uint64_t lights_seq = 0;         // bumped per rt_set_lights; a device uploads at its next frame
@@ -190,7 +194,7 @@ static void release_device(RtDevice &d)
     (void)hipSetDevice(d.device);
     for (DevBuf *b : {&d.b_cand, &d.b_cand_n, &d.b_first, &d.b_queue, &d.b_ctr, &d.b_setup, &d.b_dirs, &d.b_rgb,
                       &d.b_hit_e, &d.b_hit_n, &d.b_status, &d.b_counters, &d.b_fault, &d.b_lights, &d.b_shadow,
-                      &d.b_shadow_f, &d.b_sh, &d.b_sh_tmp, &d.b_sh_ints})
+                      &d.b_shadow_f, &d.b_sh, &d.b_sh_tmp, &d.b_sh_ints, &d.b_lmaps})
         b->release();
     for (DevBuf &b : d.b_gr) b.release();
     for (auto &e : d.ev)
@@ -283,6 +287,7 @@ extern "C" int rt_create(const rt_create_desc *desc, rt_ctx **out)
     if (const char *e = getenv("RT_STREAM_SPLIT")) c->stream_split = atoi(e) != 0;
     if (const char *e = getenv("RT_HOST_DIRECT")) c->host_direct = atoi(e) != 0;
     if (const char *e = getenv("RT_SHADOW_GRID")) c->shadow_grid = atoi(e);
+    if (const char *e = getenv("RT_LIGHT_MAP")) c->light_map = atoi(e);
     if (const char *e = getenv("RT_BANDS")) c->bands = atoi(e) < 1 ? 1 : (atoi(e) > RT_MAX_BANDS ? RT_MAX_BANDS : atoi(e));
     // gather: one part needs none; RCCL admits one rank per GPU, so a device listed twice (several
     // parts on one GPU) gathers by device copies, as RT_CREATE_PEER_GATHER asks for.  RT_GATHER
@@ -626,6 +631,37 @@ static int ensure_shadow_tree(rt_ctx *c, RtDevice &d)
     return RT_OK;
 }
 
+// The lights' direction maps on device d (rt_launch_light_map), rebuilt after a scene change or a new
+// light list; needs the shadow tree's depth array (ensure_shadow_tree first).  Synchronises d's streams
+// (and the bands' for dev[0]) before rebuilding, as ensure_shadow_tree does.
+static int ensure_light_maps(rt_ctx *c, RtDevice &d)
+{
+    const uint64_t ep = rt_store_epoch(c->store);
+    if (d.lm_epoch == ep && d.lm_seq == c->lights_seq && d.b_lmaps.p) return RT_OK;
+    int r;
+    if ((r = use_device(d)) != RT_OK) return r;
+    if (d.stream) HIP_TRY(hipStreamSynchronize(d.stream));
+    if (&d == &c->dev[0])
+        for (RtDevice &b : c->band)
+            if (b.stream) HIP_TRY(hipStreamSynchronize(b.stream));
+    auto alloc = [](void *ctx, size_t bytes, int which) -> void * {
+        DevBuf &b = static_cast<RtDevice *>(ctx)->b_gr[which];
+        return b.ensure(bytes) == RT_OK ? b.p : nullptr;
+    };
+    for (int l = 0; l < RT_MAX_LIGHTS; l++) {
+        d.lmap[l] = RtLightMap{};
+        if (l < c->n_lights && c->light_map >= 0 && d.scene.shnode &&
+            (r = rt_launch_light_map(&d.scene, (const int32_t *)d.b_sh_ints.p, c->lights[l].pos, c->light_map, alloc, &d,
+                                     4 + 4 * l, d.stream, &d.lmap[l])) != RT_OK)
+            return r;
+    }
+    if ((r = d.b_lmaps.ensure(sizeof(RtLightMap) * RT_MAX_LIGHTS)) != RT_OK) return r;
+    HIP_TRY(hipMemcpy(d.b_lmaps.p, d.lmap, sizeof(RtLightMap) * RT_MAX_LIGHTS, hipMemcpyHostToDevice));
+    d.lm_epoch = ep;
+    d.lm_seq = c->lights_seq;
+    return RT_OK;
+}
+
 // The newest completed counter copy of device d into its snapshot (the grid hints and the host-frame
 // streaming gate read it).  A frame that took a buffer but sent no counters (fused small frame, empty
 // part, an error before the copy) never records its event, and the query then reports success: the
@@ -734,7 +770,9 @@ static int prepare(rt_ctx *c, RtDevice &d, const rt_camera_desc *cam, const rt_c
         // the shadow tree belongs to the GPU's scene: a band (dev[0]'s GPU) takes dev[0]'s
         RtDevice &ph = (&d >= c->band && &d < c->band + RT_MAX_BANDS) ? c->dev[0] : d;
         if ((r = ensure_shadow_tree(c, ph)) != RT_OK) return r;
+        if ((r = ensure_light_maps(c, ph)) != RT_OK) return r;
         if ((r = use_device(d)) != RT_OK) return r;
+        L.lmaps = c->light_map >= 0 ? (const RtLightMap *)ph.b_lmaps.p : nullptr;
         d.scene.shnode = ph.scene.shnode;
         d.scene.n_sh = ph.scene.n_sh;
         d.scene.g_cell = ph.scene.g_cell;

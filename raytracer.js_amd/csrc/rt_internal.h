@@ -78,6 +78,20 @@ struct alignas(16) RtShNode {
 };
 static_assert(sizeof(RtShNode) == 32, "RtShNode must stay 32 bytes");
 
+// A point light's map of the primitives by direction (shadow rays): six faces of
+// res x res cells over the direction w = x - pos from the light.  Face 2a + (w[a] < 0) holds the
+// directions whose largest |component| is axis a; its cell is (u, v) = the other two components, in
+// axis order, over |w[a]|, each on [-1, 1] in res steps.  Cell c lists ref[cell[c] .. cell[c + 1])
+// (RtBvh: the primitive's conservative box and slot); big lists the primitives for every direction
+// (unbounded, containing the light, or over many cells).  res = 0: no map.
+struct RtLightMap {
+    const uint32_t *cell;
+    const RtBvh *ref;
+    const RtBvh *big;
+    double pos[3];
+    int32_t res, nbig;
+};
+
 // Per-node cull hierarchy: a binary BVH over one node's entity list, stored in
 // depth-first order with skip links (stackless).  Bounds are the entities' AABBs widened by a
 // margin and rounded outward to f32, so a ray that the exact binary64 test can report as hitting
@@ -283,6 +297,7 @@ struct RtLaunch {
     double *shadow_k;                           // [n_lights][rows*W]: light l's cosine * isl at record q, -1
                                                 // when it is skipped or blocked (k_shadow_rays; k_shadow
                                                 // adds rgb_l * k in light order)
+    const RtLightMap *lmaps;                    // device [RT_MAX_LIGHTS]: the lights' direction maps, or null
 };
 
 // ctr: [0] overflow count, [1] its claim head, [2] deferred matte ends (shadow rays), [3] unused; a
@@ -315,6 +330,11 @@ int rt_launch_shadow_tree(const RtDevScene &S, RtShNode *tmp, RtShNode *out, int
 typedef void *(*RtGridAlloc)(void *ctx, size_t bytes, int which);
 int rt_launch_shadow_grid(RtDevScene *S, const int32_t *depth, int res, RtGridAlloc alloc, void *alloc_ctx,
                           void *stream);
+// The direction map of a light at pos (res cells per face axis; 0: from the primitive count), built on
+// the device from the scene's primitives (depth: as above); alloc's buffers which_base + 0 .. 3 as for
+// the grid.  Writes *out (res stays 0 when the scene has no cull scale).  Synchronises `stream`.
+int rt_launch_light_map(const RtDevScene *S, const int32_t *depth, const double pos[3], int res, RtGridAlloc alloc,
+                        void *alloc_ctx, int which_base, void *stream, RtLightMap *out);
 
 // ---- multi-device frame assembly (rt_multi.hip) -------------------------------------------------------
 // Rows between a frame (H rows of row_bytes) and the stacked parts (n_parts x max_rows rows):

@@ -1421,16 +1421,59 @@ __device__ __forceinline__ bool shadow_blocked_all(const RtShNode *sh, int n_sh,
     return false;
 }
 
+// The light-map search: the light's large list, then the one cell of the direction
+// w = q - pos from the light.  A primitive the segment [q, pos] meets at h is seen from the light in
+// direction h - pos, a positive multiple of w: same face (the largest |component| and its sign), same
+// (u, v); the map lists the primitive in every cell its box's directions reach (k_lm_pass), so the
+// cell holds every primitive that can block.  Returns -1 when the map cannot place w (zero or non-
+// finite), for the grid search instead.
+__device__ __forceinline__ int shadow_blocked_lm(const RtDevScene &S, const RtLightMap &M, const RayBox &rb, float tlim,
+                                              const double q[3], const double u[3], double lim)
+{
+    const double w0 = q[0] - M.pos[0], w1 = q[1] - M.pos[1], w2 = q[2] - M.pos[2];
+    const double a0 = fabs(w0), a1 = fabs(w1), a2 = fabs(w2);
+    const int a = (a0 >= a1 && a0 >= a2) ? 0 : (a1 >= a2 ? 1 : 2);
+    const double m = a == 0 ? a0 : (a == 1 ? a1 : a2);
+    if (!(m > 0 && m < INFINITY)) return -1;
+    const double wa = a == 0 ? w0 : (a == 1 ? w1 : w2);
+    const double wb = a == 0 ? w1 : w0, wc = a == 2 ? w1 : w2;
+    const int R = M.res;
+    const double sc = 0.5 * (double)R / m;
+    int cu = (int)floor((wb + m) * sc), cv = (int)floor((wc + m) * sc);
+    cu = cu < 0 ? 0 : (cu >= R ? R - 1 : cu);
+    cv = cv < 0 ? 0 : (cv >= R ? R - 1 : cv);
+    const uint32_t cell = ((uint32_t)(2 * a + (wa < 0 ? 1 : 0)) * (uint32_t)R + (uint32_t)cv) * (uint32_t)R + (uint32_t)cu;
+    const RtBvh *arr = M.big;
+    uint32_t r = 0, re = (uint32_t)M.nbig;
+    bool in_cell = false;
+    for (;;) {
+        if (r < re) {
+            const RtBvh e = arr[r++];
+            if (ray_box_seg(e.lo, e.hi, rb, tlim) && prim_blocks(S, e.info, q, u, lim)) return 1;
+            continue;
+        }
+        if (in_cell) return 0;
+        in_cell = true;
+        arr = M.ref;
+        r = M.cell[cell];
+        re = M.cell[cell + 1];
+    }
+}
+
 // GRID_ONLY: the caller knows the scene has a grid and culling is on (k_shadow's grid instantiation)
 template <bool GRID_ONLY = false>
 __device__ __forceinline__ bool shadow_blocked(const RtDevScene &S, bool cull, const double q[3], const double u[3],
-                                            double dist)
+                                            double dist, const RtLightMap *M = nullptr)
 {
     const RayBox rb = make_raybox(q, u);
     const bool prune = cull && rb.ok;
     float tlim = (float)(dist * 1.0001);
     if (!(tlim >= 0.0f)) tlim = INFINITY;
     const double lim = dist - 1e-3;
+    if (M && prune) {
+        const int b = shadow_blocked_lm(S, *M, rb, tlim, q, u, lim);
+        if (b >= 0) return b != 0;
+    }
     if (GRID_ONLY) {
         if (rb.ok) return shadow_blocked_grid(S, rb, tlim, q, u, lim);
         return shadow_blocked_all(S.shnode, S.n_sh, S.bvh, S.prim, S.shades, q[0], q[1], q[2], u[0], u[1], u[2], lim);
@@ -2565,7 +2608,8 @@ __global__ void __launch_bounds__(256, MINW) k_shadow_rays(RtLaunch L)
         const RtShadowRec &e = L.shadow_q[q];
         const double p[3] = {e.p[0], e.p[1], e.p[2]}, nrm[3] = {e.n[0], e.n[1], e.n[2]};
         double o[3], d[3], dist, cosine, k = -1.0;             // -1: the light is skipped or blocked
-        if (shadow_ray(L.lights[l], p, nrm, o, d, dist, cosine) && !shadow_blocked<GRID>(L.scene, cull, o, d, dist)) {
+        const RtLightMap *M = L.lmaps && L.lmaps[l].res > 0 ? L.lmaps + l : nullptr;
+        if (shadow_ray(L.lights[l], p, nrm, o, d, dist, cosine) && !shadow_blocked<GRID>(L.scene, cull, o, d, dist, M)) {
             const double t = (e.path + dist) * L.cfg.distance_attenuation_factor;     // shadow_add's k
             const double isl = 1.0 / (2.220446049250313e-16 + t * t);
             k = cosine * isl;
@@ -2761,8 +2805,10 @@ __device__ __forceinline__ bool grid_range(const GridDims &G, const float lo[3],
 template <bool FILL>
 __global__ void __launch_bounds__(256) k_gr_pass(RtDevScene S, GridDims G, double delta, const int32_t *depth,
                                                 uint32_t *count, const uint32_t *start, RtBvh *ref, RtBvh *big,
-                                                int32_t *nbig)
+                                                int32_t *nbig, int32_t big_cap)
 {
+    // Fill writes only inside what the count pass sized (a cell's [start, next start), the large list's
+    // big_cap): both passes compute the same ranges, and the guard keeps it so if they ever did not.
     for (int n = blockIdx.x; n < S.n_nodes; n += gridDim.x) {
         if (depth[n] < 0) continue;                              // a slot not under the root
         const int4 ne = reinterpret_cast<const int4 *>(S.node_ent)[n];   // {prim begin, count, ...}
@@ -2775,7 +2821,7 @@ __global__ void __launch_bounds__(256) k_gr_pass(RtDevScene S, GridDims G, doubl
             int i0[3], i1[3];
             if (!grid_range(G, e.lo, e.hi, bounded, i0, i1)) {
                 const int k = atomicAdd(nbig, 1);
-                if (FILL) big[k] = e;
+                if (FILL && k < big_cap) big[k] = e;
                 continue;
             }
             for (int z = i0[2]; z <= i1[2]; z++)
@@ -2783,7 +2829,7 @@ __global__ void __launch_bounds__(256) k_gr_pass(RtDevScene S, GridDims G, doubl
                     for (int x = i0[0]; x <= i1[0]; x++) {
                         const uint32_t cell = ((uint32_t)z * (uint32_t)G.res + (uint32_t)y) * (uint32_t)G.res + (uint32_t)x;
                         const uint32_t k = atomicAdd(&count[cell], 1u);
-                        if (FILL) ref[start[cell] + k] = e;
+                        if (FILL && start[cell] + k < start[cell + 1]) ref[start[cell] + k] = e;
                     }
         }
     }
@@ -3145,6 +3191,84 @@ int rt_launch_shadow_tree(const RtDevScene &S, RtShNode *tmp, RtShNode *out, int
     return RT_OK;
 }
 
+// ---- the lights' direction maps (rt_launch_light_map) ------------------------------------------------------
+constexpr int LM_BIG_CELLS = 64;            // a primitive over more cells goes to the light's large list
+constexpr double LM_EPS = 1e-9;             // slack on a face's (u, v) bounds (the ray side errs < 1e-15)
+
+// The cells of face f that directions from the light at L through the box [lo, hi] can fall in, as
+// [u0, u1] x [v0, v1]; 0: none, 1: that range, 2: unbounded (the box reaches the light's own point).
+// Directions of face f (axis a, side s) have z = s (x[a] - L[a]) >= max(|x[b] - L[b]|, |x[c] - L[c]|)
+// > 0, so only the part of the box with z >= max(min |x[b] - L[b]|, min |x[c] - L[c]|) = zc counts;
+// clipped there, the box lies in front of the face's plane and its directions' (u, v) = (x[b] - L[b],
+// x[c] - L[c]) / z span the range of its clipped corners' (a convex set, projected).
+__device__ int lm_face_range(const float lo[3], const float hi[3], const double L[3], int f, int R, int &u0, int &u1,
+                             int &v0, int &v1)
+{
+    const int a = f >> 1;
+    const bool neg = f & 1;
+    const int b = a == 0 ? 1 : 0, c = a == 2 ? 1 : 2;
+    const double zlo = neg ? L[a] - (double)hi[a] : (double)lo[a] - L[a];
+    const double zhi = neg ? L[a] - (double)lo[a] : (double)hi[a] - L[a];
+    if (!(zhi > 0)) return 0;
+    const double x0 = (double)lo[b] - L[b], x1 = (double)hi[b] - L[b];
+    const double y0 = (double)lo[c] - L[c], y1 = (double)hi[c] - L[c];
+    const double mx = (x0 <= 0 && x1 >= 0) ? 0.0 : fmin(fabs(x0), fabs(x1));
+    const double my = (y0 <= 0 && y1 >= 0) ? 0.0 : fmin(fabs(y0), fabs(y1));
+    const double zl = fmax(zlo, fmax(mx, my));
+    if (zl > zhi) return 0;
+    if (!(zl > 0)) return 2;
+    const double umin = fmin(fmin(x0 / zl, x0 / zhi), fmin(x1 / zl, x1 / zhi)) - LM_EPS;
+    const double umax = fmax(fmax(x0 / zl, x0 / zhi), fmax(x1 / zl, x1 / zhi)) + LM_EPS;
+    const double vmin = fmin(fmin(y0 / zl, y0 / zhi), fmin(y1 / zl, y1 / zhi)) - LM_EPS;
+    const double vmax = fmax(fmax(y0 / zl, y0 / zhi), fmax(y1 / zl, y1 / zhi)) + LM_EPS;
+    if (umax < -1.0 || umin > 1.0 || vmax < -1.0 || vmin > 1.0) return 0;
+    const double k = 0.5 * (double)R;
+    auto cell = [&](double t) { const double x = floor((fmin(fmax(t, -1.0), 1.0) + 1.0) * k); return x >= R ? R - 1 : (int)x; };
+    u0 = cell(umin); u1 = cell(umax); v0 = cell(vmin); v1 = cell(vmax);
+    return 1;
+}
+
+// Pass 1 (count) / pass 2 (fill) of a light's map, as k_gr_pass for the grid: one block per node slot,
+// its threads over the node's primitives.
+template <bool FILL>
+__global__ void __launch_bounds__(256) k_lm_pass(RtDevScene S, double lx, double ly, double lz, int R, double delta,
+                                                const int32_t *depth, uint32_t *count, const uint32_t *start,
+                                                RtBvh *ref, RtBvh *big, int32_t *nbig, int32_t big_cap)
+{
+    const double L[3] = {lx, ly, lz};
+    for (int n = blockIdx.x; n < S.n_nodes; n += gridDim.x) {
+        if (depth[n] < 0) continue;
+        const int4 ne = reinterpret_cast<const int4 *>(S.node_ent)[n];
+        for (int j = threadIdx.x; j < ne.y; j += blockDim.x) {
+            const int slot = ne.x + j;
+            RtBvh e;
+            bool listed = prim_box(S.prim[slot], delta, e.lo, e.hi);
+            e.skip = 0;
+            e.info = slot;
+            int rg[6][4], kind[6], cells = 0;
+            for (int f = 0; f < 6 && listed; f++) {
+                kind[f] = lm_face_range(e.lo, e.hi, L, f, R, rg[f][0], rg[f][1], rg[f][2], rg[f][3]);
+                if (kind[f] == 2) listed = false;
+                else if (kind[f] == 1) cells += (rg[f][1] - rg[f][0] + 1) * (rg[f][3] - rg[f][2] + 1);
+            }
+            if (!listed || cells > LM_BIG_CELLS) {
+                const int k = atomicAdd(nbig, 1);
+                if (FILL && k < big_cap) big[k] = e;
+                continue;
+            }
+            for (int f = 0; f < 6; f++) {
+                if (kind[f] != 1) continue;
+                for (int v = rg[f][2]; v <= rg[f][3]; v++)
+                    for (int u = rg[f][0]; u <= rg[f][1]; u++) {
+                        const uint32_t cell = ((uint32_t)f * (uint32_t)R + (uint32_t)v) * (uint32_t)R + (uint32_t)u;
+                        const uint32_t k = atomicAdd(&count[cell], 1u);
+                        if (FILL && start[cell] + k < start[cell + 1]) ref[start[cell] + k] = e;
+                    }
+            }
+        }
+    }
+}
+
 int rt_launch_shadow_grid(RtDevScene *S, const int32_t *depth, int res, RtGridAlloc alloc, void *actx, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
@@ -3188,7 +3312,7 @@ int rt_launch_shadow_grid(RtDevScene *S, const int32_t *depth, int res, RtGridAl
     HIP_TRY(hipMemsetAsync(nbig, 0, sizeof(int32_t), st));
     const int blocks = (int)std::min<long long>(N, 1 << 16);
     hipLaunchKernelGGL(k_gr_pass<false>, dim3(blocks), dim3(256), 0, st, *S, G, delta, depth, count,
-                       (const uint32_t *)nullptr, (RtBvh *)nullptr, (RtBvh *)nullptr, nbig);
+                       (const uint32_t *)nullptr, (RtBvh *)nullptr, (RtBvh *)nullptr, nbig, 0);
     HIP_TRY(hipGetLastError());
     const int nsc = (int)(n_cells + 1);
     hipLaunchKernelGGL(k_scan_local, dim3(nb), dim3(256), 0, st, (const uint32_t *)count, start, tops, nsc);
@@ -3203,10 +3327,13 @@ int rt_launch_shadow_grid(RtDevScene *S, const int32_t *depth, int res, RtGridAl
     RtBvh *ref = (RtBvh *)alloc(actx, sizeof(RtBvh) * ((size_t)n_ref + 1), 1);
     RtBvh *big = (RtBvh *)alloc(actx, sizeof(RtBvh) * ((size_t)n_big + 1), 2);
     if (!ref || !big) return rt_set_error(RT_E_HIP, "shadow grid: out of device memory");
+    // zeroed entries (primitive slot 0, an empty box at the origin) stand in for any the fill misses
+    HIP_TRY(hipMemsetAsync(ref, 0, sizeof(RtBvh) * ((size_t)n_ref + 1), st));
+    HIP_TRY(hipMemsetAsync(big, 0, sizeof(RtBvh) * ((size_t)n_big + 1), st));
     HIP_TRY(hipMemsetAsync(count, 0, sizeof(uint32_t) * (n_cells + 1), st));
     HIP_TRY(hipMemsetAsync(nbig, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(k_gr_pass<true>, dim3(blocks), dim3(256), 0, st, *S, G, delta, depth, count,
-                       (const uint32_t *)start, ref, big, nbig);
+                       (const uint32_t *)start, ref, big, nbig, n_big);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
     S->g_cell = start;
@@ -3216,6 +3343,71 @@ int rt_launch_shadow_grid(RtDevScene *S, const int32_t *depth, int res, RtGridAl
     S->g_res = res;
     S->g_cs = G.cs;
     for (int a = 0; a < 3; a++) S->g_lo[a] = G.lo[a];
+    return RT_OK;
+}
+
+int rt_launch_light_map(const RtDevScene *S, const int32_t *depth, const double pos[3], int res, RtGridAlloc alloc,
+                        void *actx, int wb, void *stream, RtLightMap *out)
+{
+    hipStream_t st = (hipStream_t)stream;
+    *out = RtLightMap{};
+    const int N = S->n_nodes;
+    if (N <= 0 || S->n_list <= 0) return RT_OK;
+    for (int a = 0; a < 3; a++)
+        if (!std::isfinite(pos[a])) return RT_OK;
+    if (res <= 0) {
+        // about two entries per cell: 6 res^2 >= 2 list entries, a power of two from 64 to 512 per face axis
+        res = 64;
+        while (res < 512 && (double)res * res * 6 < 2.0 * (double)S->n_list) res *= 2;
+    }
+    res = std::min(512, std::max(4, res));       // 1024: see DESIGN.md §3.6
+    RtNode root;
+    HIP_TRY(hipMemcpyAsync(&root, S->node, sizeof(RtNode), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const double rp[3] = {root.x, root.y, root.z};
+    double delta = 0, clampv = 0;
+    rt_cull_scale(rp, root.s, &delta, &clampv);
+    if (!(delta > 0 && std::isfinite(delta))) return RT_OK;
+    const size_t n_cells = (size_t)6 * res * res;
+    uint32_t *count = (uint32_t *)alloc(actx, sizeof(uint32_t) * (2 * n_cells + 2), wb + 0);
+    const int nb = (int)((n_cells + 1 + SCAN_BLOCK - 1) / SCAN_BLOCK);
+    uint32_t *tops = (uint32_t *)alloc(actx, sizeof(uint32_t) * (size_t)(nb + 4), wb + 3);
+    if (!count || !tops) return rt_set_error(RT_E_HIP, "light map: out of device memory");
+    uint32_t *start = count + n_cells + 1;
+    int32_t *nbig = (int32_t *)(tops + nb + 1);
+    HIP_TRY(hipMemsetAsync(count, 0, sizeof(uint32_t) * (n_cells + 1), st));
+    HIP_TRY(hipMemsetAsync(nbig, 0, sizeof(int32_t), st));
+    const int blocks = (int)std::min<long long>(N, 1 << 16);
+    hipLaunchKernelGGL(k_lm_pass<false>, dim3(blocks), dim3(256), 0, st, *S, pos[0], pos[1], pos[2], res, delta, depth,
+                       count, (const uint32_t *)nullptr, (RtBvh *)nullptr, (RtBvh *)nullptr, nbig, 0);
+    HIP_TRY(hipGetLastError());
+    const int nsc = (int)(n_cells + 1);
+    hipLaunchKernelGGL(k_scan_local, dim3(nb), dim3(256), 0, st, (const uint32_t *)count, start, tops, nsc);
+    hipLaunchKernelGGL(k_scan_tops, dim3(1), dim3(256), 0, st, tops, nb);
+    hipLaunchKernelGGL(k_scan_add, dim3((nsc + 255) / 256), dim3(256), 0, st, start, (const uint32_t *)tops, nsc);
+    HIP_TRY(hipGetLastError());
+    uint32_t n_ref = 0;
+    int32_t n_big = 0;
+    HIP_TRY(hipMemcpyAsync(&n_ref, start + n_cells, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&n_big, nbig, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    RtBvh *ref = (RtBvh *)alloc(actx, sizeof(RtBvh) * ((size_t)n_ref + 1), wb + 1);
+    RtBvh *big = (RtBvh *)alloc(actx, sizeof(RtBvh) * ((size_t)n_big + 1), wb + 2);
+    if (!ref || !big) return rt_set_error(RT_E_HIP, "light map: out of device memory");
+    HIP_TRY(hipMemsetAsync(ref, 0, sizeof(RtBvh) * ((size_t)n_ref + 1), st));
+    HIP_TRY(hipMemsetAsync(big, 0, sizeof(RtBvh) * ((size_t)n_big + 1), st));
+    HIP_TRY(hipMemsetAsync(count, 0, sizeof(uint32_t) * (n_cells + 1), st));
+    HIP_TRY(hipMemsetAsync(nbig, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(k_lm_pass<true>, dim3(blocks), dim3(256), 0, st, *S, pos[0], pos[1], pos[2], res, delta, depth,
+                       count, (const uint32_t *)start, ref, big, nbig, n_big);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    out->cell = start;
+    out->ref = ref;
+    out->big = big;
+    out->nbig = n_big;
+    out->res = res;
+    for (int a = 0; a < 3; a++) out->pos[a] = pos[a];
     return RT_OK;
 }
 

@@ -190,14 +190,22 @@ SHADOW_CASES = [
     ("config1", (96, 64), 3, LIGHTS, 0.0, {"blend": 0.25}),
     # the search over the pre-order tree of union boxes instead of the grid (RT_SHADOW_GRID=-1), split
     # and fused; grids of 2 cells per axis (most primitives in the large list) and of 256 (each
-    # primitive over many cells, some over more than the cell limit)
-    ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "-1"}}),
-    ("config1", (160, 120), 3, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "-1"}}),
+    # primitive over many cells, some over more than the cell limit); the lights' direction maps off
+    # (RT_LIGHT_MAP=-1) so that the grid and the tree answer
+    ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "-1", "RT_LIGHT_MAP": "-1"}}),
+    ("config1", (160, 120), 3, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "-1", "RT_LIGHT_MAP": "-1"}}),
     ("small7", (128, 96), 4, LIGHTS, 0.1, {}),
-    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "-1"}}),
-    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "2"}}),
-    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "256"}}),
-    ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "3"}}),
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "-1", "RT_LIGHT_MAP": "-1"}}),
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "2", "RT_LIGHT_MAP": "-1"}}),
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "256", "RT_LIGHT_MAP": "-1"}}),
+    ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "3", "RT_LIGHT_MAP": "-1"}}),
+    # the lights' direction maps (the default): 4 cells per face axis (most cells shared by many
+    # primitives), 512 (the largest; primitives near a light over more than the cell limit, in its
+    # large list), a light inside a sphere and one on a triangle's vertex (in the large list: the box
+    # holds the light)
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": dict(SPLIT, RT_LIGHT_MAP="4")}),
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": dict(SPLIT, RT_LIGHT_MAP="512")}),
+    ("small4", (128, 96), 4, "inside", 0.1, {"env": SPLIT}),
 ]
 
 
@@ -208,6 +216,13 @@ def test_shadow_rays_equal_oracle(monkeypatch, name, wh, refmax, lights, ambient
         monkeypatch.setenv(k, v)                      # read at rt_create
     spec = {"config1": scenes.config1_spheres, "small4": lambda: scenes.small_random(4),
             "small7": lambda: scenes.small_random(7, n_tri=600, half=0.05)}[name]()
+    if lights == "inside":
+        # a light at a sphere's centre and one on a triangle's first vertex (plus a free one)
+        ents = spec.entities
+        sph = ents[ents["type"] == abi.RT_ENT_SPHERE][0]
+        tri = ents[ents["type"] == abi.RT_ENT_FACE][0]
+        lights = [(tuple(float(x) for x in sph["geom"][:3]), (0.6, 0.5, 0.4)),
+                  (tuple(float(x) for x in tri["geom"][:3]), (0.3, 0.4, 0.9)), LIGHTS[2]]
     cam = scenes.make_camera(*wh)
     blend = opt.get("blend")
     cfg = scenes.make_config(refmax, col_weight=blend if blend else 1.0)
