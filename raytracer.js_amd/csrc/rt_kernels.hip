@@ -3192,7 +3192,7 @@ int rt_launch_shadow_tree(const RtDevScene &S, RtShNode *tmp, RtShNode *out, int
 }
 
 // ---- the lights' direction maps (rt_launch_light_map) ------------------------------------------------------
-constexpr int LM_BIG_CELLS = 64;            // a primitive over more cells goes to the light's large list
+constexpr int LM_BIG_CELLS = 1024;          // a primitive over more cells goes to the light's large list (RT_LM_BIG)
 constexpr double LM_EPS = 1e-9;             // slack on a face's (u, v) bounds (the ray side errs < 1e-15)
 
 // The cells of face f that directions from the light at L through the box [lo, hi] can fall in, as
@@ -3233,7 +3233,7 @@ __device__ int lm_face_range(const float lo[3], const float hi[3], const double 
 template <bool FILL>
 __global__ void __launch_bounds__(256) k_lm_pass(RtDevScene S, double lx, double ly, double lz, int R, double delta,
                                                 const int32_t *depth, uint32_t *count, const uint32_t *start,
-                                                RtBvh *ref, RtBvh *big, int32_t *nbig, int32_t big_cap)
+                                                RtBvh *ref, RtBvh *big, int32_t *nbig, int32_t big_cap, int big_cells)
 {
     const double L[3] = {lx, ly, lz};
     for (int n = blockIdx.x; n < S.n_nodes; n += gridDim.x) {
@@ -3251,7 +3251,7 @@ __global__ void __launch_bounds__(256) k_lm_pass(RtDevScene S, double lx, double
                 if (kind[f] == 2) listed = false;
                 else if (kind[f] == 1) cells += (rg[f][1] - rg[f][0] + 1) * (rg[f][3] - rg[f][2] + 1);
             }
-            if (!listed || cells > LM_BIG_CELLS) {
+            if (!listed || cells > big_cells) {
                 const int k = atomicAdd(nbig, 1);
                 if (FILL && k < big_cap) big[k] = e;
                 continue;
@@ -3361,6 +3361,7 @@ int rt_launch_light_map(const RtDevScene *S, const int32_t *depth, const double 
         while (res < 512 && (double)res * res * 6 < 2.0 * (double)S->n_list) res *= 2;
     }
     res = std::min(512, std::max(4, res));       // 1024: see DESIGN.md §3.6
+    const int big_cells = getenv("RT_LM_BIG") ? std::max(1, atoi(getenv("RT_LM_BIG"))) : LM_BIG_CELLS;
     RtNode root;
     HIP_TRY(hipMemcpyAsync(&root, S->node, sizeof(RtNode), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -3379,7 +3380,7 @@ int rt_launch_light_map(const RtDevScene *S, const int32_t *depth, const double 
     HIP_TRY(hipMemsetAsync(nbig, 0, sizeof(int32_t), st));
     const int blocks = (int)std::min<long long>(N, 1 << 16);
     hipLaunchKernelGGL(k_lm_pass<false>, dim3(blocks), dim3(256), 0, st, *S, pos[0], pos[1], pos[2], res, delta, depth,
-                       count, (const uint32_t *)nullptr, (RtBvh *)nullptr, (RtBvh *)nullptr, nbig, 0);
+                       count, (const uint32_t *)nullptr, (RtBvh *)nullptr, (RtBvh *)nullptr, nbig, 0, big_cells);
     HIP_TRY(hipGetLastError());
     const int nsc = (int)(n_cells + 1);
     hipLaunchKernelGGL(k_scan_local, dim3(nb), dim3(256), 0, st, (const uint32_t *)count, start, tops, nsc);
@@ -3399,7 +3400,7 @@ int rt_launch_light_map(const RtDevScene *S, const int32_t *depth, const double 
     HIP_TRY(hipMemsetAsync(count, 0, sizeof(uint32_t) * (n_cells + 1), st));
     HIP_TRY(hipMemsetAsync(nbig, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(k_lm_pass<true>, dim3(blocks), dim3(256), 0, st, *S, pos[0], pos[1], pos[2], res, delta, depth,
-                       count, (const uint32_t *)start, ref, big, nbig, n_big);
+                       count, (const uint32_t *)start, ref, big, nbig, n_big, big_cells);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
     out->cell = start;

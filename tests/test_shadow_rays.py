@@ -200,11 +200,12 @@ SHADOW_CASES = [
     ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "256", "RT_LIGHT_MAP": "-1"}}),
     ("small4", (128, 96), 4, LIGHTS, 0.1, {"env": {"RT_SHADOW_GRID": "3", "RT_LIGHT_MAP": "-1"}}),
     # the lights' direction maps (the default): 4 cells per face axis (most cells shared by many
-    # primitives), 512 (the largest; primitives near a light over more than the cell limit, in its
-    # large list), a light inside a sphere and one on a triangle's vertex (in the large list: the box
+    # primitives), 512 (the largest), a large-list limit of 4 cells (most primitives in the lights'
+    # large lists), a light inside a sphere and one on a triangle's vertex (in the large list: the box
     # holds the light)
     ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": dict(SPLIT, RT_LIGHT_MAP="4")}),
     ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": dict(SPLIT, RT_LIGHT_MAP="512")}),
+    ("small7", (128, 96), 4, LIGHTS, 0.1, {"env": dict(SPLIT, RT_LM_BIG="4")}),
     ("small4", (128, 96), 4, "inside", 0.1, {"env": SPLIT}),
 ]
 
