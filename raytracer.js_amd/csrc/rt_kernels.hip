@@ -2519,8 +2519,8 @@ __global__ void __launch_bounds__(256, MINW) k_shade(RtLaunch L)
     const bool queued = L.level == 0;             // level 0: the rays k_first queued
     const int n_q = queued ? *shade_n(L) : 0;
     const int n_it = queued ? (n_q + 63) >> 6 : items;
-    // level 0's queue (with lights: every primary ray, ~30 k items at 1080p) is dealt out by wave: its
-    // grid from the hints has about two waves per item, and a claim each serialised on one atomic
+    // level 0's queue (the rays early_shade did not end) is dealt out by wave: its grid from the hints
+    // has about two waves per item, and a claim each serialised on one atomic
     const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)), waves = (int)(gridDim.x * (blockDim.x >> 6));
     int next = wave;
     for (;;) {
