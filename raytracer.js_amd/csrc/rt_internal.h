@@ -293,7 +293,7 @@ struct RtLaunch {
     double ambient;
     const rt_light *lights;
     RtShadowRec *shadow_q;                      // split path with lights: [rows*W] deferred matte ends
-                                                // (count ctr[2], k_shadow's claim head ctr[3]), else null
+                                                // (count ctr[RT_CTR_SHN], on its own line), else null
     double *shadow_k;                           // [n_lights][rows*W]: light l's cosine * isl at record q, -1
                                                 // when it is skipped or blocked (k_shadow_rays; k_shadow
                                                 // adds rgb_l * k in light order)
@@ -306,7 +306,7 @@ struct RtLaunch {
 // Then per level the walk pass's 8 per-XCD claim heads, one cache line each (k_walk_first with
 // RT_XCD bit 0, k_walk_refill).
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_SH = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1),
-       RT_CTR_XW = RT_CTR_SH + 8 * 32, RT_CTR_HOST = RT_CTR_XW, RT_CTR_INTS = RT_CTR_XW + 256 * (RT_MAX_LEVELS + 1) };
+       RT_CTR_SHN = RT_CTR_SH + 8 * 32, RT_CTR_XW = RT_CTR_SHN + 32, RT_CTR_HOST = RT_CTR_XW, RT_CTR_INTS = RT_CTR_XW + 256 * (RT_MAX_LEVELS + 1) };
 
 // walk_wait / walk_done (host-frame bands): the level-0 walk pass waits for event walk_wait (the
 // previous band's level-0 walk) and walk_done is recorded after it, so bands' walks run in order.

@@ -1526,11 +1526,12 @@ __device__ __forceinline__ void shadow_factor(const RtDevScene &S, const RtLaunc
     }
 }
 
-// Split path with lights: the matte end of a ray, deferred to k_shadow (count L.ctr[2]).
+// Split path with lights: the matte end of a ray, deferred to k_shadow (count L.ctr[RT_CTR_SHN], alone on
+// its cache line: the level's shading waves reserve there while other passes' counters move).
 __device__ __forceinline__ void shadow_push(const RtLaunch &L, const double p[3], const double n[3], double col0,
                                             double col1, double col2, double path, const RayResult &R, int pix)
 {
-    const int k = wave_reserve(L.ctr + 2);
+    const int k = wave_reserve(L.ctr + RT_CTR_SHN);
     RtShadowRec &e = L.shadow_q[k];
     e.p[0] = p[0]; e.p[1] = p[1]; e.p[2] = p[2];
     e.n[0] = n[0]; e.n[1] = n[1]; e.n[2] = n[2];
@@ -2579,7 +2580,7 @@ __global__ void __launch_bounds__(256, MINW) k_cont(RtLaunch L)
 }
 
 // Shadow rays on the split path (rt_set_lights): the matte ends the frame's passes
-// deferred (L.shadow_q, count ctr[2]).  k_shadow_rays takes one (light, record) pair per lane, light
+// deferred (L.shadow_q, count ctr[RT_CTR_SHN]).  k_shadow_rays takes one (light, record) pair per lane, light
 // by light (64 consecutive records toward one light per wave: neighbouring pixels, coherent searches)
 // and writes the light's k = cosine * isl for the record (-1: skipped or blocked); k_shadow then adds
 // rgb_l * k in light order (shadow_add's operations) and writes the pixels.  A lane carries one search
@@ -2590,7 +2591,7 @@ __global__ void __launch_bounds__(256, MINW) k_shadow_rays(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
-    const int n = L.ctr[2], nl = L.n_lights;
+    const int n = L.ctr[RT_CTR_SHN], nl = L.n_lights;
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     const long long items = (long long)n * nl;
     const int n_it = (int)((items + 63) >> 6);
@@ -2624,7 +2625,7 @@ __global__ void __launch_bounds__(256, MINW) k_shadow(RtLaunch L)
 {
     TL_SCOPE(L.tl);
     const int lane = threadIdx.x & 63;
-    const int n = L.ctr[2];
+    const int n = L.ctr[RT_CTR_SHN];
     const size_t stride = (size_t)L.rows * (size_t)L.cam.width;
     // uniform work: the records dealt out by wave, no claims
     const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)), waves = (int)(gridDim.x * (blockDim.x >> 6));
