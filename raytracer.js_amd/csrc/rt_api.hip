@@ -1213,7 +1213,7 @@ static int trace_frame_stream(rt_ctx *c, const rt_camera_desc *cam, const rt_con
     // frame again
     const int32_t *h = L.ctr_hint;
     const bool halves = c->stream_split && L.walk_first;
-    const long long late_hint = h && h[4] >= 0 && h[0] >= 0 && h[5] >= 0 ? (long long)h[4] + h[0] + (halves ? h[5] : 0) : -1;
+    const long long late_hint = h && h[4] >= 0 && h[0] >= 0 && h[RT_CTR_SHADE0] >= 0 ? (long long)h[4] + h[0] + (halves ? h[RT_CTR_SHADE0] : 0) : -1;
     const long long cap = c->late_cap > 0 ? c->late_cap
                         : std::min<long long>((long long)P, std::max(1ll << 16, 2 * std::max(0ll, late_hint)));
     if ((r = d0.b_rgb.ensure(sizeof(float) * 3 * P)) != RT_OK) return r;

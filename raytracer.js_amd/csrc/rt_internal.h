@@ -306,7 +306,8 @@ struct RtLaunch {
 // Then per level the walk pass's 8 per-XCD claim heads, one cache line each (k_walk_first with
 // RT_XCD bit 0, k_walk_refill).
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_SH = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1),
-       RT_CTR_SHN = RT_CTR_SH + 8 * 32, RT_CTR_XW = RT_CTR_SHN + 32, RT_CTR_HOST = RT_CTR_XW, RT_CTR_INTS = RT_CTR_XW + 256 * (RT_MAX_LEVELS + 1) };
+       RT_CTR_SHN = RT_CTR_SH + 8 * 32, RT_CTR_SHADE0 = RT_CTR_SHN + 32, RT_CTR_XW = RT_CTR_SHN + 64,
+       RT_CTR_HOST = RT_CTR_XW, RT_CTR_INTS = RT_CTR_XW + 256 * (RT_MAX_LEVELS + 1) };
 
 // walk_wait / walk_done (host-frame bands): the level-0 walk pass waits for event walk_wait (the
 // previous band's level-0 walk) and walk_done is recorded after it, so bands' walks run in order.

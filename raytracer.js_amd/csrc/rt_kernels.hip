@@ -1905,9 +1905,10 @@ __device__ __forceinline__ void ray_src(const RtLaunch &L, int item, int lane, R
     }
 }
 
-// Level 0's shading queue (k_first -> k_shade): its length, in a free slot of the
-// level's counter block; the entries (pixel ids of this part) live in ray_cn, unused at level 0.
-__device__ __forceinline__ int32_t *shade_n(const RtLaunch &L) { return lvl_ctr(L, 0) + 1; }
+// Level 0's shading queue (k_first -> k_shade): its length, alone on a cache line (the first-hit
+// pass reserves there while its waves claim work); the entries (pixel ids of this part) live in
+// ray_cn, unused at level 0.
+__device__ __forceinline__ int32_t *shade_n(const RtLaunch &L) { return L.ctr + RT_CTR_SHADE0; }
 
 // The primary ray of pixel `id` of this part (row-major within the part), as ray_src gives it.
 __device__ __forceinline__ void pixel_src(const RtLaunch &L, int id, RaySrc &r)
@@ -3067,9 +3068,9 @@ int rt_launch_frame(const RtLaunch &L, void *stream, void *ev_begin, void *ev_en
             // costs time, and a small part's frame no longer dispatches full grids that do nothing.
             int mb_plain = mb, mb_seg = mb, mb_refill = mb, mb_first = mb, mb_shade = mb;
             int mb_seg_shade = mb, mb_seg_wide = mb;
-            if (lv == 0 && L.shade_hint && L.ctr_hint && L.ctr_hint[5] >= 0) {
+            if (lv == 0 && L.shade_hint && L.ctr_hint && L.ctr_hint[RT_CTR_SHADE0] >= 0) {
                 // level 0's shading queue of a recent frame (shade_n): 64 rays per work item, 2x headroom
-                const long long items = ((long long)L.ctr_hint[5] + 63) / 64;
+                const long long items = ((long long)L.ctr_hint[RT_CTR_SHADE0] + 63) / 64;
                 mb_shade = (int)std::min<long long>(std::max<long long>(8, (2 * items + 3) / 4), 1 << 20);
             }
             if (lv >= 1 && hint >= 0 && RT_NO_OP_BLOCKS > 0) {
