@@ -300,14 +300,16 @@ struct RtLaunch {
     const RtLightMap *lmaps;                    // device [RT_MAX_LIGHTS]: the lights' direction maps, or null
 };
 
-// ctr: [0] overflow count, [1] its claim head, [2] deferred matte ends (shadow rays), [3] unused; a
-// block of RT_CTR_LEVEL per bounce level from 4; then k_shadow_rays' 8 claim heads, 32 ints apart (one
-// cache line each).  The first RT_CTR_HOST ints come back to the host after a frame (grid hints).
-// Then per level the walk pass's 8 per-XCD claim heads, one cache line each (k_walk_first with
-// RT_XCD bit 0, k_walk_refill).
+// ctr: [0] overflow count, [1] its claim head, [2], [3] unused; a block of RT_CTR_LEVEL per bounce
+// level from 4 (its queue count first); k_shadow_rays' 8 claim heads, 32 ints apart (one cache line
+// each); the deferred matte ends' count and level 0's shading-queue count, one line each.  The first
+// RT_CTR_HOST ints come back to the host after a frame (grid hints).  Then per level the walk pass's 8
+// per-XCD claim heads, one cache line each (k_walk_first with RT_XCD bit 0, k_walk_refill), and per
+// level and pass (walk, first-hit, shade) its 8 claim heads on a line of their own (pass_heads).
 enum { RT_MAX_LEVELS = 32, RT_CTR_LEVEL = 32, RT_CTR_SH = 4 + RT_CTR_LEVEL * (RT_MAX_LEVELS + 1),
        RT_CTR_SHN = RT_CTR_SH + 8 * 32, RT_CTR_SHADE0 = RT_CTR_SHN + 32, RT_CTR_XW = RT_CTR_SHN + 64,
-       RT_CTR_HOST = RT_CTR_XW, RT_CTR_INTS = RT_CTR_XW + 256 * (RT_MAX_LEVELS + 1) };
+       RT_CTR_HOST = RT_CTR_XW, RT_CTR_PH = RT_CTR_XW + 256 * (RT_MAX_LEVELS + 1),
+       RT_CTR_INTS = RT_CTR_PH + 32 * 3 * (RT_MAX_LEVELS + 1) };
 
 // walk_wait / walk_done (host-frame bands): the level-0 walk pass waits for event walk_wait (the
 // previous band's level-0 walk) and walk_done is recorded after it, so bands' walks run in order.

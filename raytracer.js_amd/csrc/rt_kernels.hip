@@ -1796,12 +1796,15 @@ __device__ __forceinline__ void write_pixel(const RtLaunch &L, size_t pix, const
 // ---- work distribution ------------------------------------------------------------------------------------
 // Device counters (L.ctr): [0] overflow queue count, [1] its read head; per level lv (0 = primary
 // rays, >= 1 = continuation levels) a block of RT_CTR_LEVEL at 4 + RT_CTR_LEVEL*lv: [0] the count
-// of the queue written at this level, [8p .. 8p+7] the per-XCD work heads of pass p (1 k_walk,
-// 2 k_first, 3 k_shade).  Level lv reads queue (lv-1)&1 and writes queue lv&1.
+// of the queue written at this level; the passes' claim heads are elsewhere (pass_heads).  Level lv
+// reads queue (lv-1)&1 and writes queue lv&1.
 __device__ __forceinline__ int32_t *lvl_ctr(const RtLaunch &L, int lv) { return L.ctr + 4 + RT_CTR_LEVEL * lv; }
 
 // The 8 per-XCD claim heads of pass p (1 walk, 2 first, 3 shade) at level lv.
-__device__ __forceinline__ int32_t *pass_heads(const RtLaunch &L, int lv, int p) { return lvl_ctr(L, lv) + 8 * p; }
+__device__ __forceinline__ int32_t *pass_heads(const RtLaunch &L, int lv, int p)
+{
+    return L.ctr + RT_CTR_PH + 32 * (3 * lv + p - 1);     // off the level's count line (its queue pushes)
+}
 
 // Level lv's walk-pass heads on separate cache lines (claim_xcd with hs = 32): a wave claims with a
 // returning atomic, and those on one line serialise (~15 ns each), which several thousand waves
