@@ -3365,7 +3365,9 @@ int rt_launch_light_map(const RtDevScene *S, const int32_t *depth, const double 
         res = 64;
         while (res < 512 && (double)res * res * 6 < 2.0 * (double)S->n_list) res *= 2;
     }
-    res = std::min(512, std::max(4, res));       // 1024: see DESIGN.md §3.6
+    // at most 512 per face axis (RT_LM_MAX raises it for diagnosis; 1024: see DESIGN.md §3.6)
+    const int res_max = getenv("RT_LM_MAX") ? std::max(4, atoi(getenv("RT_LM_MAX"))) : 512;
+    res = std::min(res_max, std::max(4, res));
     const int big_cells = getenv("RT_LM_BIG") ? std::max(1, atoi(getenv("RT_LM_BIG"))) : LM_BIG_CELLS;
     RtNode root;
     HIP_TRY(hipMemcpyAsync(&root, S->node, sizeof(RtNode), hipMemcpyDeviceToHost, st));
